@@ -1,0 +1,128 @@
+/*
+ * libwhisper_hip — C ABI of the MI355X (gfx950) Whisper backend.
+ *
+ * This is the drop-in replacement for the reference's native backend boundary,
+ * coreml/coreml.h:5-31 of wangchou/whisper.coreml, which Python binds through
+ * ctypes in whisper/coreml.py:19-244.  The roles map one to one (citations are
+ * /root/reference paths):
+ *
+ *   loadEncoder/loadCrossKV/loadDecoder256/loadDecoder1 (coreml.h:5,9,13,23)
+ *        -> wh_create + wh_load_tensor + wh_finalize (weights come from the
+ *           reference's own state_dict names, whisper/__init__.py:152-160)
+ *   encoderPredict (coreml.h:7) + crossKVPredict (coreml.h:11)
+ *        -> wh_encode  (AudioEncoder.forward encoder.py:103-136 and
+ *           TextDecoder.crossKVCaches decoder.py:172-187, all windows batched)
+ *   decoder256Predict (coreml.h:15-21) -> wh_decode_begin (first pass) /
+ *           wh_prefill_logits (full-row logits + alignment cross-QK)
+ *   decoder1Predict (coreml.h:26-31) + rearrange_mkv (coreml.h:25) + the host
+ *           beam/filter loop (whisper/decoding.py:707-737)
+ *        -> wh_decode_steps (one hipGraph per token: decoder step, logit filters,
+ *           greedy/beam update, KV reorder by index indirection)
+ *   log_mel_spectrogram (whisper/audio.py:110-157) -> wh_log_mel
+ *   showCoremlPredictTime (whisper/coreml.py:247-263) -> wh_stats
+ *
+ * Conventions: every call returns 0 on success, a negative code on failure
+ * (message via wh_last_error, thread-local).  All pointers are host pointers
+ * (plain C arrays, row-major); device memory is owned by the context.  A
+ * context is bound to one HIP device; use one context per GPU process.
+ */
+#ifndef WHISPER_HIP_H
+#define WHISPER_HIP_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct wh_ctx wh_ctx;
+
+/* ModelDimensions (whisper/model.py:18-29) */
+typedef struct wh_dims {
+  int n_mels, n_audio_ctx, n_audio_state, n_audio_head, n_audio_layer;
+  int n_vocab, n_text_ctx, n_text_state, n_text_head, n_text_layer;
+} wh_dims;
+
+enum { WH_F32 = 0, WH_F16 = 1 };
+
+/* DecodingOptions (whisper/decoding.py:81-115) resolved against the tokenizer */
+typedef struct wh_decode_opts {
+  int group;             /* rows per window: beam_size, best_of or 1 (<= 8) */
+  int beam;              /* 1 = BeamSearchDecoder, 0 = GreedyDecoder */
+  float patience;        /* beam: max_candidates = round(group * patience) */
+  float temperature;     /* greedy: 0 = argmax, > 0 = sampling */
+  int sample_len;        /* max updates (n_text_ctx / 2 by default) */
+  int suppress_blank;    /* SuppressBlank */
+  int timestamps;        /* ApplyTimestampRules (0 = without_timestamps) */
+  int max_initial;       /* max_initial_timestamp index, -1 = none */
+  int eot, no_speech, no_timestamps, timestamp_begin; /* no_speech < 0: none */
+  int blank[4];          /* tokenizer.encode(" ") ids suppressed with eot at the first step */
+  int n_blank;
+  const int* suppress;   /* SuppressTokens ids (already resolved, -1 expanded) */
+  int n_suppress;
+  unsigned long long seed; /* sampling RNG seed */
+} wh_decode_opts;
+
+const char* wh_last_error(void);
+int wh_version(void);
+
+int wh_create(int device, const wh_dims* dims, int compute_dtype, int max_windows, int max_group, wh_ctx** out);
+int wh_destroy(wh_ctx* ctx);
+
+/* checkpoint-format float32 tensor by reference state_dict name; the decoder query
+   pre-scale (decoder.py:16-20) and the encoder key scale (encoder.py:38) are
+   folded here. */
+int wh_load_tensor(wh_ctx* ctx, const char* name, const float* data, const int64_t* shape, int ndim);
+int wh_finalize(wh_ctx* ctx);
+
+/* mel filterbank [n_mels][201] (whisper/audio.py:91-107; the host derives it with the
+   Slaney formula librosa uses and checks it against the reference asset in tests) */
+int wh_set_mel_filters(wh_ctx* ctx, int n_mels, const float* filters);
+
+/* log-mel of a whole file into the context's mel buffer: n_frames = (n + padding) / 160.
+   normalize = 1 applies the global-max floor and scaling immediately. */
+int wh_log_mel(wh_ctx* ctx, const float* audio, int64_t n_samples, int64_t padding, int n_mels, int normalize,
+               int64_t* n_frames);
+int wh_mel_max(wh_ctx* ctx, float* gmax);              /* raw log10 max of the last wh_log_mel */
+int wh_mel_normalize(wh_ctx* ctx, float gmax);         /* floor at gmax-8, (x+4)/4 */
+int wh_mel_read(wh_ctx* ctx, float* out, int64_t frame0, int64_t n_frames); /* [n_mels][n_frames] */
+int wh_mel_write(wh_ctx* ctx, const float* mel, int64_t n_frames);          /* host mel -> context */
+
+/* encoder + cross-KV for n_win windows of the context mel: window i = frames
+   [seek[i], seek[i] + seg[i]) zero-padded to 3000 (audio.py:65-88), into slot i */
+int wh_encode(wh_ctx* ctx, int n_win, const int64_t* seek_frames, const int* seg_frames);
+int wh_read_audio_features(wh_ctx* ctx, int slot, float* out);                   /* [n_audio_ctx][n_state] */
+int wh_read_cross_kv(wh_ctx* ctx, int slot, int layer, float* k_out, float* v_out); /* [H][n_audio_ctx][64] */
+
+/* decode n_win windows (slots 0..n_win-1): prefill of the initial tokens
+   (init_tokens[w*max_init + i], i < n_init[w]) and the first token update */
+int wh_decode_begin(wh_ctx* ctx, int n_win, const wh_decode_opts* opts, const int* init_tokens, const int* n_init,
+                    int max_init, const int* sot_index);
+/* run up to max_steps token updates (hipGraph); *n_done = windows finished */
+int wh_decode_steps(wh_ctx* ctx, int max_steps, int* n_done);
+/* read back a window: tokens [group][n_text_ctx+1], sum_logprobs [group], len,
+   finished (beam) fin_tokens [maxc][n_text_ctx+1], fin_len/fin_score [maxc] */
+int wh_decode_read(wh_ctx* ctx, int slot, int* tokens, float* sum_logprobs, int* len, int* fin_n, int* fin_tokens,
+                   int* fin_len, float* fin_score, float* no_speech_prob);
+int wh_decode_maxc(wh_ctx* ctx);
+
+/* decoder forward over tokens at offset 0 for one window slot (Whisper.forward,
+   model.py:110-119 / the decoder256 first pass); logits [n_tokens][n_vocab];
+   align_qk (nullable) [n_align][n_tokens][n_audio_ctx] raw cross q.k of the heads
+   in align_heads (layer*n_head + head) */
+int wh_prefill_logits(wh_ctx* ctx, int slot, const int* tokens, int n_tokens, float* logits, const int* align_heads,
+                      int n_align, float* align_qk);
+
+/* cumulative stage wall times in ms: [0] mel [1] encode [2] prefill [3] steps
+   [4] step count [5] encode windows */
+int wh_stats(wh_ctx* ctx, double* out, int n);
+int wh_sync(wh_ctx* ctx);
+
+/* timing of the dominant kernels for roofline reporting: runs `iters` launches of
+   the given stage on the context's own stream between HIP events.
+   what: 0 = one decoder step graph (current batch), 1 = encoder of 1 window */
+int wh_time_stage(wh_ctx* ctx, int what, int iters, double* ms_per_iter);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,352 @@
+"""Golden-vector generator: runs the REFERENCE (/root/reference) on seeded inputs.
+
+TEST INFRASTRUCTURE ONLY.  This script is run by hand in the survey/build
+container, where /root/reference exists.  It imports the reference fork's own
+``whisper`` package (CPU PyTorch path, ``use_coreml=False``) with two
+stand-in modules for the absent third-party packages (oracle/standins/:
+``tiktoken`` = plain BPE, ``numba`` = identity ``jit``) and
+writes small fixtures to tests/golden/.  Nothing from the reference travels:
+only inputs (as seeds) and outputs (as arrays).
+
+Weights come from whisper.coreml_amd/whisper/synthetic.py (our own seeded
+generator, loaded by file path so it does not clash with the reference's
+``whisper`` package); the GPU box regenerates the identical weights.
+
+Usage:  python oracle/gen_golden.py [micro tiny.en turbo large-v3 mel tokens dtw]
+"""
+
+import importlib.util
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(HERE)
+OUT = os.path.join(REPO, "tests", "golden")
+REF = "/root/reference"
+
+sys.path.insert(0, REF)
+sys.path.insert(0, os.path.join(HERE, "standins"))
+
+import torch  # noqa: E402
+
+torch.set_num_threads(os.cpu_count() or 8)
+
+import whisper as refw  # noqa: E402  (the REFERENCE package)
+from whisper import audio as ref_audio  # noqa: E402
+from whisper import decoding as ref_decoding  # noqa: E402
+from whisper import timing as ref_timing  # noqa: E402
+from whisper import tokenizer as ref_tok  # noqa: E402
+from whisper.model import ModelDimensions, Whisper  # noqa: E402
+
+assert os.path.realpath(os.path.dirname(refw.__file__)).startswith(REF), refw.__file__
+
+_spec = importlib.util.spec_from_file_location(
+    "wh_synthetic", os.path.join(REPO, "whisper.coreml_amd", "whisper", "synthetic.py"))
+syn = importlib.util.module_from_spec(_spec)
+_spec.loader.exec_module(syn)
+
+N_SAMPLES = ref_audio.N_SAMPLES
+
+
+def build_ref_model(name: str, seed: int = 0):
+    dims = syn.MODEL_DIMS[name]
+    sd = syn.synthetic_state_dict(dims, seed)
+    model = Whisper(ModelDimensions(**dims), False, name)
+    ref_keys = set(model.state_dict().keys())
+    assert ref_keys == set(sd.keys()), (ref_keys ^ set(sd.keys()))
+    model.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()})
+    if name in refw._ALIGNMENT_HEADS:
+        model.set_alignment_heads(refw._ALIGNMENT_HEADS[name])
+    model.eval()
+    return model, sd
+
+
+class MarginRecorder:
+    """Wraps GreedyDecoder.update to record the post-filter top-2 margin per step."""
+
+    def __init__(self):
+        self.margins = []
+        self._orig = ref_decoding.GreedyDecoder.update
+        rec = self
+
+        def update(this, tokens, logits, sum_logprobs):
+            top2 = torch.topk(logits.float(), 2, dim=-1).values
+            rec.margins.append((top2[:, 0] - top2[:, 1]).tolist())
+            return rec._orig(this, tokens, logits, sum_logprobs)
+
+        ref_decoding.GreedyDecoder.update = update
+
+    def close(self):
+        ref_decoding.GreedyDecoder.update = self._orig
+
+
+def pack_result(prefix: str, r, out: dict):
+    out[f"{prefix}_tokens"] = np.asarray(r.tokens, dtype=np.int32)
+    out[f"{prefix}_avg_logprob"] = np.float64(r.avg_logprob)
+    out[f"{prefix}_no_speech_prob"] = np.float64(r.no_speech_prob)
+
+
+def topk_pack(prefix: str, row: torch.Tensor, out: dict, k: int = 64):
+    v, i = torch.topk(row.float(), k)
+    out[f"{prefix}_topv"] = v.numpy().astype(np.float32)
+    out[f"{prefix}_topi"] = i.numpy().astype(np.int32)
+    out[f"{prefix}_lse"] = np.float64(torch.logsumexp(row.double(), 0).item())
+    out[f"{prefix}_mean"] = np.float64(row.double().mean().item())
+    out[f"{prefix}_std"] = np.float64(row.double().std().item())
+
+
+def model_goldens(name: str, seed: int = 0, audio_seed: int = 1, full: bool = False,
+                  beam_natural: bool = True):
+    t0 = time.time()
+    model, sd = build_ref_model(name, seed)
+    dims = syn.MODEL_DIMS[name]
+    out = {"seed": np.int32(seed), "audio_seed": np.int32(audio_seed),
+           "weights_checksum": np.float64(syn.state_dict_checksum(sd))}
+    del sd
+    lang_opts = dict(language="en", fp16=False)
+    audio = syn.synthetic_audio(30.0, seed=audio_seed)
+    mel = ref_audio.log_mel_spectrogram(audio, dims["n_mels"], padding=N_SAMPLES)
+    mel_seg = ref_audio.pad_or_trim(mel[:, :3000], 3000)
+    out["mel_window_sum"] = np.float64(mel_seg.double().sum().item())
+    with torch.no_grad():
+        xa = model.encoder(mel_seg.unsqueeze(0))[0]
+        out["xa_rownorm"] = xa.double().norm(dim=1).numpy()
+        out["xa_head"] = xa[:64].numpy().astype(np.float32)
+        out["xa_tail"] = xa[-64:].numpy().astype(np.float32)
+        if full:
+            out["xa_full"] = xa.numpy().astype(np.float32)
+        ck, cv = model.decoder.crossKVCaches(xa.unsqueeze(0))
+        # ck: (L, H, 64, 1500); cv: (L, H, 1500, 64)
+        out["ck_norm"] = ck.double().norm(dim=(2, 3)).numpy()
+        out["cv_norm"] = cv.double().norm(dim=(2, 3)).numpy()
+        out["ck_slice"] = ck[:, :, :, :32].numpy().astype(np.float32)
+        tok = refw.tokenizer.get_tokenizer(model.is_multilingual, num_languages=model.num_languages,
+                                           language="en", task="transcribe")
+        sot = list(tok.sot_sequence)
+        out["sot_sequence"] = np.asarray(sot, dtype=np.int32)
+        logits, cross_qks, _ = model.decoder(torch.tensor([sot]), xa.unsqueeze(0), 0, None)
+        topk_pack("first_last", logits[0, -1], out)
+        topk_pack("first_sot", logits[0, 0], out)
+        if full:
+            out["first_last_full"] = logits[0, -1].numpy().astype(np.float32)
+        # a prompt-conditioned first pass (sequential transcribe mode, decoding.py:628-638)
+        prompt = [tok.sot_prev] + list(range(1000, 1040)) + sot
+        out["prompt_tokens"] = np.asarray(prompt, dtype=np.int32)
+        model.decoder.cross_k_caches = None
+        logits_p, _, _ = model.decoder(torch.tensor([prompt]), xa.unsqueeze(0), 0, None)
+        topk_pack("prompt_last", logits_p[0, -1], out)
+    print(f"[{name}] encoder+first pass {time.time()-t0:.1f}s", flush=True)
+
+    # greedy, natural
+    rec = MarginRecorder()
+    r = refw.decode(model, mel_seg, ref_decoding.DecodingOptions(temperature=0.0, **lang_opts))
+    rec.close()
+    pack_result("greedy", r, out)
+    out["greedy_margins"] = np.asarray([m[0] for m in rec.margins], dtype=np.float32)
+    print(f"[{name}] greedy natural {len(r.tokens)} tok {time.time()-t0:.1f}s", flush=True)
+    # greedy, fixed work (EOT suppressed -> 224 steps)
+    eot = tok.eot
+    rec = MarginRecorder()
+    r = refw.decode(model, mel_seg, ref_decoding.DecodingOptions(
+        temperature=0.0, suppress_tokens=f"-1,{eot}", **lang_opts))
+    rec.close()
+    pack_result("greedy_fixed", r, out)
+    out["greedy_fixed_margins"] = np.asarray([m[0] for m in rec.margins], dtype=np.float32)
+    print(f"[{name}] greedy fixed {len(r.tokens)} tok {time.time()-t0:.1f}s", flush=True)
+    # greedy with a prompt
+    r = refw.decode(model, mel_seg, ref_decoding.DecodingOptions(
+        temperature=0.0, prompt=list(range(1000, 1040)), **lang_opts))
+    pack_result("greedy_prompt", r, out)
+    # beam search
+    if beam_natural:
+        r = refw.decode(model, mel_seg, ref_decoding.DecodingOptions(temperature=0.0, beam_size=5, **lang_opts))
+        pack_result("beam", r, out)
+        print(f"[{name}] beam natural {len(r.tokens)} tok {time.time()-t0:.1f}s", flush=True)
+    r = refw.decode(model, mel_seg, ref_decoding.DecodingOptions(
+        temperature=0.0, beam_size=5, suppress_tokens=f"-1,{eot}", **lang_opts))
+    pack_result("beam_fixed", r, out)
+    print(f"[{name}] beam fixed {len(r.tokens)} tok {time.time()-t0:.1f}s", flush=True)
+    # without timestamps (sot_sequence_including_notimestamps)
+    r = refw.decode(model, mel_seg, ref_decoding.DecodingOptions(
+        temperature=0.0, without_timestamps=True, **lang_opts))
+    pack_result("greedy_notime", r, out)
+    return model, out
+
+
+def transcribe_goldens(model, name: str, out: dict):
+    """transcribe() on 35 s + 65 s audio: sharded mode and sequential mode."""
+    segs_all = {}
+    audio = syn.synthetic_audio(65.0, seed=7)
+    runs = {
+        "clip_beam": dict(beam_size=5, condition_on_previous_text=False, clip_timestamps="0,30,30,60,60"),
+        "clip_greedy": dict(condition_on_previous_text=False, clip_timestamps="0,30,30,60,60"),
+        "seq_greedy": dict(condition_on_previous_text=True),
+        "seq_beam": dict(beam_size=5, condition_on_previous_text=True),
+    }
+    for key, kw in runs.items():
+        t0 = time.time()
+        res = refw.transcribe(model, audio, temperature=0.0, language="en", fp16=False, verbose=None, **kw)
+        segs_all[key] = [
+            dict(seek=s["seek"], start=s["start"], end=s["end"], tokens=s["tokens"],
+                 avg_logprob=s["avg_logprob"], no_speech_prob=s["no_speech_prob"],
+                 temperature=s["temperature"])
+            for s in res["segments"]]
+        print(f"[{name}] transcribe {key}: {len(res['segments'])} segs {time.time()-t0:.1f}s", flush=True)
+    with open(os.path.join(OUT, f"{name}_transcribe.json"), "w") as f:
+        json.dump(dict(audio_seconds=65.0, audio_seed=7, runs=runs, segments=segs_all), f, indent=0)
+
+
+def mel_goldens():
+    out = {}
+    out["filters_80"] = ref_audio.mel_filters("cpu", 80).numpy()
+    out["filters_128"] = ref_audio.mel_filters("cpu", 128).numpy()
+    cases = [("a", 1.0, 11, 80, 0), ("b", 2.0, 12, 128, 0), ("c", 31.5, 13, 128, N_SAMPLES),
+             ("d", 30.0, 14, 80, N_SAMPLES), ("e", 0.5, 15, 80, 0), ("f", 600.0, 16, 128, N_SAMPLES)]
+    meta = []
+    for tag, sec, seed, nm, pad in cases:
+        audio = syn.synthetic_audio(sec, seed=seed)
+        m = ref_audio.log_mel_spectrogram(audio, nm, padding=pad).numpy()
+        meta.append(dict(tag=tag, seconds=sec, seed=seed, n_mels=nm, padding=pad, frames=int(m.shape[1])))
+        if m.shape[1] <= 256:
+            out[f"{tag}_full"] = m
+        else:
+            for lo, hi in [(0, 48), (m.shape[1] // 2 - 8, m.shape[1] // 2 + 8), (m.shape[1] - 3016, m.shape[1] - 2984),
+                           (m.shape[1] - 16, m.shape[1])]:
+                out[f"{tag}_{lo}"] = m[:, lo:hi]
+        out[f"{tag}_max"] = np.float64(m.max())
+        out[f"{tag}_sum"] = np.float64(m.astype(np.float64).sum())
+        out[f"{tag}_colsum"] = m.astype(np.float64).sum(axis=0)
+    out["meta"] = np.asarray(json.dumps(meta))
+    np.savez_compressed(os.path.join(OUT, "mel.npz"), **out)
+    print("mel goldens:", [m["frames"] for m in meta])
+
+
+def _is_ws(b: bytes) -> bool:
+    try:
+        return b.decode("utf-8").strip() == ""
+    except UnicodeDecodeError:
+        return False
+
+
+def token_goldens():
+    res = {}
+    for multilingual, nl in [(True, 100), (True, 99), (False, 99)]:
+        tok = ref_tok.get_tokenizer(multilingual, num_languages=nl, language="en", task="transcribe")
+        key = f"{'multilingual' if multilingual else 'gpt2'}_{nl}"
+        res[key] = dict(
+            eot=tok.eot, sot=tok.sot, translate=tok.translate, transcribe=tok.transcribe,
+            sot_lm=tok.sot_lm, sot_prev=tok.sot_prev, no_speech=tok.no_speech,
+            no_timestamps=tok.no_timestamps, timestamp_begin=tok.timestamp_begin,
+            sot_sequence=list(tok.sot_sequence), non_speech_tokens=list(tok.non_speech_tokens),
+            blank=tok.encode(" "), n_vocab=tok.encoding.n_vocab,
+            all_language_tokens=list(tok.all_language_tokens),
+            fellow=tok.encode(" And so my fellow Americans"),
+            # ids whose decoded text is whitespace only: transcribe.py:494-499 clears
+            # segments whose text .strip() == "" (needs no BPE decoder with this list)
+            whitespace_tokens=sorted(i for b, i in tok.encoding._ranks.items()
+                                     if _is_ws(b)),
+        )
+    with open(os.path.join(OUT, "tokens.json"), "w") as f:
+        json.dump(res, f, indent=0)
+    print("token goldens:", {k: len(v["non_speech_tokens"]) for k, v in res.items()})
+
+
+def planted_dtw(N, M, rng):
+    """Same construction as reference tests/test_timing.py:22-49 (own seeded rng)."""
+    steps = np.concatenate([np.zeros(N - 1), np.ones(M - 1)])
+    rng.shuffle(steps)
+    x = rng.random((N, M)).astype(np.float32)
+    i, j, k = 0, 0, 0
+    trace = []
+    while True:
+        x[i, j] -= 1
+        trace.append((i, j))
+        if k == len(steps):
+            break
+        if k + 1 < len(steps) and steps[k] != steps[k + 1]:
+            i += 1
+            j += 1
+            k += 2
+            continue
+        if steps[k] == 0:
+            i += 1
+        if steps[k] == 1:
+            j += 1
+        k += 1
+    return x, np.array(trace).T
+
+
+def dtw_goldens():
+    out = {}
+    rng = np.random.default_rng(42)
+    for N, M in [(10, 20), (32, 16), (123, 1500), (234, 189)]:
+        x, trace = planted_dtw(N, M, rng)
+        out[f"planted_{N}x{M}_x"] = x
+        out[f"planted_{N}x{M}_trace"] = trace.astype(np.int32)
+        got = ref_timing.dtw_cpu(x.astype(np.float64))
+        assert np.array_equal(got, trace), (N, M)
+    for N, M in [(8, 40), (57, 300), (120, 750)]:
+        x = rng.standard_normal((N, M)).astype(np.float32)
+        out[f"rand_{N}x{M}_x"] = x
+        out[f"rand_{N}x{M}_path"] = np.asarray(ref_timing.dtw_cpu(x.astype(np.float64)), dtype=np.int32)
+    for shape in [(10,), (1, 15), (4, 5, 345), (2, 3, 20, 100)]:
+        x = rng.standard_normal(shape).astype(np.float32)
+        for w in (3, 5, 7, 13):
+            key = "x".join(map(str, shape))
+            out[f"med_{key}_x"] = x
+            out[f"med_{key}_w{w}"] = ref_timing.median_filter(torch.from_numpy(x), w).numpy()
+    np.savez_compressed(os.path.join(OUT, "dtw.npz"), **out)
+    print("dtw goldens:", len(out))
+
+
+def asset_export():
+    """Product asset (data only): language codes in token order and, per
+    vocabulary, the special ids / SuppressTokens(-1) list / whitespace-only ids
+    that tokenizer.py:132-327 computes with tiktoken.  Written to
+    whisper.coreml_amd/whisper/assets/specials.json."""
+    langs = list(ref_tok.LANGUAGES.items())
+    res = {"languages": [[c, n] for c, n in langs], "to_language_code": dict(ref_tok.TO_LANGUAGE_CODE),
+           "vocab": {}}
+    for multilingual in (True, False):
+        for nl in range(99, 101):
+            tok = ref_tok.get_tokenizer(multilingual, num_languages=nl)
+            key = f"{'multilingual' if multilingual else 'gpt2'}_{nl}"
+            res["vocab"][key] = dict(
+                n_base=len(tok.encoding._ranks), n_vocab=tok.encoding.n_vocab,
+                non_speech_tokens=list(tok.non_speech_tokens), blank=tok.encode(" "),
+                whitespace_tokens=sorted(i for b, i in tok.encoding._ranks.items() if _is_ws(b)))
+    out = os.path.join(REPO, "whisper.coreml_amd", "whisper", "assets")
+    os.makedirs(out, exist_ok=True)
+    with open(os.path.join(out, "specials.json"), "w") as f:
+        json.dump(res, f)
+    print("assets exported")
+
+
+def main(argv):
+    os.makedirs(OUT, exist_ok=True)
+    what = argv or ["tokens", "mel", "dtw", "micro", "tiny.en", "turbo", "large-v3"]
+    for w in what:
+        if w == "tokens":
+            token_goldens()
+        elif w == "mel":
+            mel_goldens()
+        elif w == "dtw":
+            dtw_goldens()
+        elif w == "assets":
+            asset_export()
+        else:
+            small = w.startswith("micro")
+            big = w in ("turbo", "large-v3", "large-v3-turbo")
+            model, out = model_goldens(w, full=small, beam_natural=not big)
+            np.savez_compressed(os.path.join(OUT, f"{w}.npz"), **out)
+            if small:
+                transcribe_goldens(model, w, out)
+            del model
+
+
+if __name__ == "__main__":
+    main(sys.argv[1:])

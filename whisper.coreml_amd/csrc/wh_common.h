@@ -1,0 +1,99 @@
+// Common device/host helpers for libwhisper_hip (gfx950 / CDNA4 only).
+//
+// Element types: the hot path is templated on T in {float, half_t}.  half_t is
+// the fp16 production path (weights + activations fp16, fp32 accumulate, fp32
+// residual stream); float is the parity path that matches the reference CPU
+// fp32 model token-for-token.
+//
+// MFMA fragment convention used by every GEMM / attention kernel here
+// (16x16 output tiles, wave64):
+//   lane l, row index r = l & 15, k-group g = l >> 4
+//   a "k-step" covers 32 consecutive k; lane (r, g) holds the 8 elements
+//   k = 32*s + 8*g + j (j = 0..7) of its row.
+//   * half_t : one v_mfma_f32_16x16x32_f16 per k-step
+//   * float  : eight v_mfma_f32_16x16x4_f32 per k-step, step j feeding k = 8g + j
+//     (the k order inside a step is permuted identically for A and B, so the
+//     sum is the same contraction).
+//   D layout (both): lane holds D[row = 4*g + j][col = r], j = 0..3.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+typedef _Float16 half_t;
+typedef _Float16 half8_t __attribute__((ext_vector_type(8)));
+typedef _Float16 half4_t __attribute__((ext_vector_type(4)));
+typedef float float4_t __attribute__((ext_vector_type(4)));
+typedef float float8_t __attribute__((ext_vector_type(8)));
+
+#define WH_DEV __device__ __forceinline__
+
+// ---------------------------------------------------------------- fragments
+template <typename T> struct Frag;
+template <> struct Frag<half_t> { half8_t v; };
+template <> struct Frag<float> { float8_t v; };
+
+// load 8 consecutive elements (16 B for half, 32 B for float)
+WH_DEV void frag_load(Frag<half_t>& f, const half_t* p) { f.v = *reinterpret_cast<const half8_t*>(p); }
+WH_DEV void frag_load(Frag<float>& f, const float* p) {
+  const float4_t* q = reinterpret_cast<const float4_t*>(p);
+  float4_t a = q[0], b = q[1];
+  f.v = (float8_t){a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+}
+
+WH_DEV void mfma_step(float4_t& acc, const Frag<half_t>& a, const Frag<half_t>& b) {
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(a.v, b.v, acc, 0, 0, 0);
+}
+WH_DEV void mfma_step(float4_t& acc, const Frag<float>& a, const Frag<float>& b) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.v[j], b.v[j], acc, 0, 0, 0);
+}
+
+// ---------------------------------------------------------------- conversions
+template <typename T> WH_DEV T from_f32(float x);
+template <> WH_DEV float from_f32<float>(float x) { return x; }
+template <> WH_DEV half_t from_f32<half_t>(float x) { return (half_t)x; }
+WH_DEV float to_f32(float x) { return x; }
+WH_DEV float to_f32(half_t x) { return (float)x; }
+
+// store 4 consecutive elements
+WH_DEV void store4(float* p, float a, float b, float c, float d) {
+  *reinterpret_cast<float4_t*>(p) = (float4_t){a, b, c, d};
+}
+WH_DEV void store4(half_t* p, float a, float b, float c, float d) {
+  *reinterpret_cast<half4_t*>(p) = (half4_t){(half_t)a, (half_t)b, (half_t)c, (half_t)d};
+}
+WH_DEV float4_t load4f(const float* p) { return *reinterpret_cast<const float4_t*>(p); }
+WH_DEV float4_t load4f(const half_t* p) {
+  half4_t h = *reinterpret_cast<const half4_t*>(p);
+  return (float4_t){(float)h[0], (float)h[1], (float)h[2], (float)h[3]};
+}
+
+// exact-erf GELU (nn.GELU() default), evaluated in fp32
+WH_DEV float gelu_f(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752440f)); }
+
+// ---------------------------------------------------------------- wave reductions (wave64)
+WH_DEV float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+WH_DEV float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// ordered float <-> uint for atomicMax over signed floats
+WH_DEV unsigned f2ord(float f) {
+  unsigned u = __float_as_uint(f);
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+WH_DEV float ord2f(unsigned u) { return __uint_as_float((u & 0x80000000u) ? (u & 0x7fffffffu) : ~u); }
+
+// XCD-aware bijective block remap (cdna_hip_programming.md §5 "XCD swizzle must be
+// bijective"): blocks dealt round-robin over 8 XCDs get contiguous tile ranges.
+WH_DEV int xcd_remap(int bid, int nwg) {
+  if (nwg < 16) return bid;
+  const int q = nwg / 8, r = nwg % 8, xcd = bid % 8, idx = bid / 8;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + idx;
+}

@@ -1,0 +1,401 @@
+// Device-side token selection: logit filters, log-softmax, greedy/beam update.
+//
+// Restates, as fixed-shape kernels that can live inside the per-token hipGraph,
+// the host-side Python of the reference's decode loop:
+//   SuppressBlank / SuppressTokens / ApplyTimestampRules  (whisper/decoding.py:450-532)
+//   GreedyDecoder.update                                  (decoding.py:304-320)
+//   BeamSearchDecoder.update incl. finished bookkeeping   (decoding.py:350-409)
+//   PyTorchInference.rearrange_kv_cache                   (decoding.py:189-204) -> index indirection
+// k_logit_rows: one 1024-thread workgroup per decoder row (row held in registers).
+// k_merge     : one workgroup per window (candidate merge, history/ancestry update).
+#include "wh_kernels.h"
+
+namespace wh {
+
+constexpr int LR_THREADS = 1024;
+constexpr int LR_NPT = 56;  // values per thread: V <= 57344
+constexpr int KC = 9;       // candidates kept per row (beam + 1 <= 9)
+
+struct BlockRed {
+  float v[16];
+  int i[16];
+};
+
+__device__ __forceinline__ bool better(float a, int ia, float b, int ib) { return a > b || (a == b && ia < ib); }
+
+__device__ float block_max(float x, BlockRed& sm) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  x = wave_max(x);
+  __syncthreads();
+  if (lane == 0) sm.v[wv] = x;
+  __syncthreads();
+  float r = sm.v[0];
+  for (int k = 1; k < (int)(blockDim.x >> 6); ++k) r = fmaxf(r, sm.v[k]);
+  return r;
+}
+__device__ float block_sum(float x, BlockRed& sm) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  x = wave_sum(x);
+  __syncthreads();
+  if (lane == 0) sm.v[wv] = x;
+  __syncthreads();
+  float r = 0.f;
+  for (int k = 0; k < (int)(blockDim.x >> 6); ++k) r += sm.v[k];
+  return r;
+}
+// (value desc, index asc) argbest across the block
+__device__ void block_argbest(float& v, int& idx, BlockRed& sm) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float ov = __shfl_xor(v, o, 64);
+    const int oi = __shfl_xor(idx, o, 64);
+    if (better(ov, oi, v, idx)) { v = ov; idx = oi; }
+  }
+  __syncthreads();
+  if (lane == 0) { sm.v[wv] = v; sm.i[wv] = idx; }
+  __syncthreads();
+  v = sm.v[0];
+  idx = sm.i[0];
+  for (int k = 1; k < (int)(blockDim.x >> 6); ++k)
+    if (better(sm.v[k], sm.i[k], v, idx)) { v = sm.v[k]; idx = sm.i[k]; }
+}
+
+__device__ __forceinline__ unsigned long long splitmix64(unsigned long long z) {
+  z += 0x9e3779b97f4a7c15ull;
+  z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+  z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+  return z ^ (z >> 31);
+}
+
+__global__ __launch_bounds__(LR_THREADS) void k_logit_rows(const float* __restrict__ logits, int ldl, DecState s,
+                                                           DecOpts o) {
+  __shared__ BlockRed sm;
+  __shared__ int info[8];
+  const int r = blockIdx.x, w = r / s.G;
+  const int tid = threadIdx.x;
+  if (s.done[w]) return;
+  const int len = s.len[w], sb = s.sample_begin[w];
+  const int* hist = s.hist + (int64_t)r * s.hctx;
+  const int V = o.V, tb = o.ts_begin;
+  if (tid == 0) {
+    const int nseq = len - sb;
+    const int last_ts = nseq >= 1 && hist[len - 1] >= tb;
+    const int penult_ts = nseq < 2 || hist[len - 2] >= tb;
+    int ts_last = -1;
+    for (int p = len - 1; p >= sb; --p)
+      if (hist[p] >= tb) { ts_last = hist[p]; break; }
+    info[0] = last_ts;
+    info[1] = penult_ts;
+    info[2] = ts_last;
+    info[3] = (len == sb);
+  }
+  __syncthreads();
+  const int last_ts = info[0], penult_ts = info[1], ts_last = info[2], first = info[3];
+  // mask intervals [lo, hi)
+  int mlo[4], mhi[4];
+  int nm = 0;
+  if (o.timestamps) {
+    if (last_ts) {
+      if (penult_ts) { mlo[nm] = tb; mhi[nm++] = V; }
+      else { mlo[nm] = 0; mhi[nm++] = o.eot; }
+    }
+    if (ts_last >= 0) {
+      mlo[nm] = tb;
+      mhi[nm++] = (last_ts && !penult_ts) ? ts_last : ts_last + 1;
+    }
+    if (first) {
+      mlo[nm] = 0; mhi[nm++] = tb;
+      if (o.max_initial >= 0) { mlo[nm] = tb + o.max_initial + 1; mhi[nm++] = V; }
+    }
+  }
+  const float* row = logits + (int64_t)r * ldl;
+  float x[LR_NPT];
+#pragma unroll
+  for (int k = 0; k < LR_NPT; ++k) {
+    const int i = tid + LR_THREADS * k;
+    float v = -INFINITY;
+    if (i < V) {
+      v = row[i];
+      bool kill = false;
+      if (first && o.suppress_blank)
+        for (int b = 0; b < o.n_blank; ++b) kill |= (i == o.blank[b]);
+      if (o.suppress && ((o.suppress[i >> 5] >> (i & 31)) & 1u)) kill = true;
+      if (o.timestamps) {
+        kill |= (i == o.no_ts);
+        for (int q = 0; q < nm; ++q) kill |= (i >= mlo[q] && i < mhi[q]);
+      }
+      if (kill) v = -INFINITY;
+    }
+    x[k] = v;
+  }
+  if (o.timestamps) {
+    // ApplyTimestampRules tail: if logsumexp(logprobs[tb:]) > max(logprobs[:tb]) mask text
+    float m = -INFINITY;
+#pragma unroll
+    for (int k = 0; k < LR_NPT; ++k) m = fmaxf(m, x[k]);
+    m = block_max(m, sm);
+    float se = 0.f;
+#pragma unroll
+    for (int k = 0; k < LR_NPT; ++k) se += __expf(x[k] - m);
+    const float lS0 = logf(block_sum(se, sm));
+    float mts = -INFINITY, mtx = -INFINITY;
+#pragma unroll
+    for (int k = 0; k < LR_NPT; ++k) {
+      const int i = tid + LR_THREADS * k;
+      const float lp = (x[k] - m) - lS0;
+      if (i >= tb && i < V) mts = fmaxf(mts, lp);
+      if (i < tb) mtx = fmaxf(mtx, lp);
+    }
+    mts = block_max(mts, sm);
+    mtx = block_max(mtx, sm);
+    float st = 0.f;
+    if (mts > -INFINITY) {
+#pragma unroll
+      for (int k = 0; k < LR_NPT; ++k) {
+        const int i = tid + LR_THREADS * k;
+        if (i >= tb && i < V) st += __expf(((x[k] - m) - lS0) - mts);
+      }
+    }
+    st = block_sum(st, sm);
+    const float ts_lp = mts > -INFINITY ? mts + logf(st) : -INFINITY;
+    if (ts_lp > mtx) {
+#pragma unroll
+      for (int k = 0; k < LR_NPT; ++k)
+        if (tid + LR_THREADS * k < tb) x[k] = -INFINITY;
+    }
+  }
+  // final log_softmax
+  float m = -INFINITY;
+#pragma unroll
+  for (int k = 0; k < LR_NPT; ++k) m = fmaxf(m, x[k]);
+  m = block_max(m, sm);
+  float se = 0.f;
+#pragma unroll
+  for (int k = 0; k < LR_NPT; ++k) se += __expf(x[k] - m);
+  const float logS = logf(block_sum(se, sm));
+  float* cv = s.cand_val + (int64_t)r * KC;
+  int* ci = s.cand_idx + (int64_t)r * KC;
+  if (!o.beam) {
+    float bv = -INFINITY;
+    int bi = 0x7fffffff;
+    if (o.temperature > 0.f) {
+      const unsigned long long key = splitmix64(o.seed ^ ((unsigned long long)r << 40) ^ ((unsigned long long)len << 20));
+#pragma unroll
+      for (int k = 0; k < LR_NPT; ++k) {
+        const int i = tid + LR_THREADS * k;
+        if (i >= V || x[k] == -INFINITY) continue;
+        const unsigned long long z = splitmix64(key + (unsigned long long)i);
+        const float u = ((float)(z >> 40) + 0.5f) * (1.0f / 16777216.0f);
+        const float gsc = x[k] / o.temperature - logf(-logf(u));
+        if (better(gsc, i, bv, bi)) { bv = gsc; bi = i; }
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < LR_NPT; ++k) {
+        const int i = tid + LR_THREADS * k;
+        if (i < V && better(x[k], i, bv, bi)) { bv = x[k]; bi = i; }
+      }
+    }
+    block_argbest(bv, bi, sm);
+    // logprob of the chosen token: log_softmax(logits)[tok] (decoding.py:312-313)
+    if (tid == bi % LR_THREADS) {
+      const int kk = bi / LR_THREADS;
+      float xv = -INFINITY;
+#pragma unroll
+      for (int k = 0; k < LR_NPT; ++k)
+        if (k == kk) xv = x[k];
+      ci[0] = bi;
+      cv[0] = (xv - m) - logS;
+    }
+    return;
+  }
+  // beam: top-(G+1) of the log-probabilities (value desc, index asc)
+  const int need = s.G + 1;
+  float lv[KC];
+  int li[KC];
+#pragma unroll
+  for (int q = 0; q < KC; ++q) { lv[q] = -INFINITY; li[q] = 0x7fffffff; }
+#pragma unroll
+  for (int k = 0; k < LR_NPT; ++k) {
+    const int i = tid + LR_THREADS * k;
+    if (i >= V) continue;
+    float v = x[k];
+    int vi = i;
+#pragma unroll
+    for (int q = 0; q < KC; ++q) {
+      if (q < need && better(v, vi, lv[q], li[q])) {
+        const float tv = lv[q]; const int ti = li[q];
+        lv[q] = v; li[q] = vi; v = tv; vi = ti;
+      }
+    }
+  }
+  int head = 0;
+  for (int q = 0; q < need; ++q) {
+    float hv = -INFINITY;
+    int hi = 0x7fffffff;
+#pragma unroll
+    for (int z = 0; z < KC; ++z)
+      if (z == head) { hv = lv[z]; hi = li[z]; }
+    float bv = hv;
+    int bi = hi;
+    block_argbest(bv, bi, sm);
+    if (bi == hi && hv == bv && bi != 0x7fffffff) ++head;
+    if (tid == 0) {
+      cv[q] = (bv - m) - logS;
+      ci[q] = bi;
+    }
+  }
+}
+
+void launch_logit_rows(const float* logits, int ldl, const DecState& s, const DecOpts& o, int nwin, hipStream_t st) {
+  k_logit_rows<<<nwin * s.G, LR_THREADS, 0, st>>>(logits, ldl, s, o);
+}
+
+// ------------------------------------------------------------ merge (one workgroup per window)
+constexpr int MG_MAXG = 8;
+constexpr int MG_MAXCTX = 449;
+__global__ __launch_bounds__(256) void k_merge(DecState s, DecOpts o) {
+  __shared__ int oh[MG_MAXG][MG_MAXCTX];
+  __shared__ int oa[MG_MAXG][MG_MAXCTX];
+  __shared__ int src[MG_MAXG], tok[MG_MAXG], fsrc[MG_MAXG * KC];
+  __shared__ float fsc[MG_MAXG * KC];
+  __shared__ int nfin_new, completed;
+  const int w = blockIdx.x, tid = threadIdx.x;
+  if (s.done[w]) return;
+  const int G = s.G, len = s.len[w], sb = s.sample_begin[w];
+  int* hist = s.hist + (int64_t)w * G * s.hctx;
+  int* anc = s.anc + (int64_t)w * G * s.ctx;
+  if (!o.beam) {
+    if (tid < G) {
+      const int r = w * G + tid;
+      const int last = hist[tid * s.hctx + len - 1];
+      int t = s.cand_idx[r * KC];
+      if (last == o.eot) t = o.eot;
+      else s.sum_lp[r] += s.cand_val[r * KC];
+      hist[tid * s.hctx + len] = t;
+    }
+    __syncthreads();
+    if (tid == 0) {
+      int all_eot = 1;
+      for (int b = 0; b < G; ++b) all_eot &= (hist[b * s.hctx + len] == o.eot);
+      s.len[w] = len + 1;
+      const int st = s.step[w] + 1;
+      s.step[w] = st;
+      if (all_eot || len + 1 > o.n_ctx || st >= o.sample_len) s.done[w] = 1;
+    }
+    return;
+  }
+  // stage old histories / ancestry
+  for (int i = tid; i < G * len; i += 256) {
+    const int b = i / len, p = i - b * len;
+    oh[b][p] = hist[b * s.hctx + p];
+    int a = (p < s.ctx) ? anc[b * s.ctx + p] : 0;
+    if (p == len - 1 && p >= sb) a = b;  // this step's KV of beam b was written in slot b
+    oa[b][p] = a;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    // candidates in insertion order: beam-major, top-k order (decoding.py:366-373);
+    // at the first update all beams are identical: dict keys collapse onto beam 0's
+    // candidates with the source of the last duplicate (G-1).
+    float csc[MG_MAXG * KC];
+    int csrc[MG_MAXG * KC], ctok[MG_MAXG * KC], order[MG_MAXG * KC];
+    int nc = 0;
+    const bool first = (len == sb);
+    const int nbeams = first ? 1 : G;
+    for (int b = 0; b < nbeams; ++b) {
+      const int r = w * G + b;
+      for (int k = 0; k < G + 1; ++k) {
+        csc[nc] = s.sum_lp[r] + s.cand_val[r * KC + k];
+        ctok[nc] = s.cand_idx[r * KC + k];
+        csrc[nc] = first ? (G - 1) : b;
+        order[nc] = nc;
+        ++nc;
+      }
+    }
+    // stable sort by score desc (insertion sort keeps insertion order on ties)
+    for (int i = 1; i < nc; ++i) {
+      const int t = order[i];
+      int j = i - 1;
+      while (j >= 0 && csc[order[j]] < csc[t]) { order[j + 1] = order[j]; --j; }
+      order[j + 1] = t;
+    }
+    int saved = 0, nf = 0;
+    for (int q = 0; q < nc && saved < G; ++q) {
+      const int c = order[q];
+      if (ctok[c] == o.eot) {
+        fsc[nf] = csc[c];
+        fsrc[nf] = csrc[c];
+        ++nf;
+      } else {
+        src[saved] = csrc[c];
+        tok[saved] = ctok[c];
+        s.sum_lp[w * G + saved] = csc[c];
+        ++saved;
+      }
+    }
+    nfin_new = nf;
+  }
+  __syncthreads();
+  // new histories / ancestry
+  for (int i = tid; i < G * (len + 1); i += 256) {
+    const int j = i / (len + 1), p = i - j * (len + 1);
+    hist[j * s.hctx + p] = (p < len) ? oh[src[j]][p] : tok[j];
+    if (p < len && p < s.ctx) anc[j * s.ctx + p] = oa[src[j]][p];
+  }
+  // finished sequences (already in descending order)
+  int fin0 = s.fin_n[w];
+  const int nadd = min(nfin_new, max(0, s.maxc - fin0));
+  for (int i = tid; i < nadd * (len + 1); i += 256) {
+    const int f = i / (len + 1), p = i - f * (len + 1);
+    s.fin_tok[((int64_t)w * s.maxc + fin0 + f) * s.hctx + p] = (p < len) ? oh[fsrc[f]][p] : o.eot;
+  }
+  if (tid < nadd) {
+    s.fin_score[w * s.maxc + fin0 + tid] = fsc[tid];
+    s.fin_len[w * s.maxc + fin0 + tid] = len + 1;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    const int fn = fin0 + nadd;
+    s.fin_n[w] = fn;
+    s.len[w] = len + 1;
+    const int st = s.step[w] + 1;
+    s.step[w] = st;
+    if (fn >= s.maxc || len + 1 > o.n_ctx || st >= o.sample_len) s.done[w] = 1;
+  }
+}
+
+void launch_merge(const DecState& s, const DecOpts& o, int nwin, hipStream_t st) {
+  k_merge<<<nwin, 256, 0, st>>>(s, o);
+}
+
+// ------------------------------------------------------------ no_speech prob (decoding.py:716-720)
+__global__ __launch_bounds__(256) void k_no_speech(const float* logits, int ldl, int V, int ns, float* out) {
+  __shared__ BlockRed sm;
+  const float* row = logits + (int64_t)blockIdx.x * ldl;
+  float m = -INFINITY;
+  for (int i = threadIdx.x; i < V; i += 256) m = fmaxf(m, row[i]);
+  m = block_max(m, sm);
+  float se = 0.f;
+  for (int i = threadIdx.x; i < V; i += 256) se += __expf(row[i] - m);
+  se = block_sum(se, sm);
+  if (threadIdx.x == 0) out[blockIdx.x] = __expf(row[ns] - m) / se;
+}
+void launch_no_speech(const float* logits, int ldl, int rows, int V, int ns, float* out, hipStream_t st) {
+  if (rows > 0) k_no_speech<<<rows, 256, 0, st>>>(logits, ldl, V, ns, out);
+}
+
+__global__ void k_broadcast_rows(const float* src, int ld_src, const int* src_rows, float* dst, int ld_dst, int G,
+                                 int V) {
+  const int r = blockIdx.x, w = r / G;
+  const float* s = src + (int64_t)src_rows[w] * ld_src;
+  float* d = dst + (int64_t)r * ld_dst;
+  for (int i = threadIdx.x; i < V; i += 256) d[i] = s[i];
+}
+void launch_broadcast_rows(const float* src, int ld_src, const int* src_rows, float* dst, int ld_dst, int G, int nwin,
+                           int V, hipStream_t st) {
+  k_broadcast_rows<<<nwin * G, 256, 0, st>>>(src, ld_src, src_rows, dst, ld_dst, G, V);
+}
+
+}  // namespace wh

@@ -1,0 +1,83 @@
+// GEMM argument block and fused epilogues (see wh_gemm.hip).
+#pragma once
+#include "wh_common.h"
+
+namespace wh {
+
+enum Epi {
+  EPI_STORE = 0,       // out[T]  = acc + bias
+  EPI_STORE_GELU = 1,  // out[T]  = gelu(acc + bias)
+  EPI_RESID = 2,       // out_f32 += acc + bias            (residual stream, in place)
+  EPI_GELU_POS = 3,    // out_f32  = gelu(acc + bias) + pos[row-in-group]   (conv2 -> x)
+  EPI_HEADSPLIT = 4,   // cross-KV: out[(l2, win, head, t, d)] = acc + bias
+  EPI_QKV_DEC = 5,     // decoder q -> out[T]; k,v -> self-KV cache at (win, slot, head, pos)
+  EPI_F32_COLS = 6,    // logits: out_f32[m][n] (ragged N)
+};
+
+struct GemmArgs {
+  const void* X = nullptr;  // [M rows] x K, element (m,k) at X + grp*x_group_stride + rowInGrp*ldx + k
+  const void* W = nullptr;  // [N][K]
+  const float* bias = nullptr;
+  int M = 0, N = 0, K = 0;
+  int ldx = 0;
+  int x_group_rows = 1 << 30;     // rows per group (windows); M for a plain matrix
+  int64_t x_group_stride = 0;     // elements between groups
+  // outputs
+  void* out = nullptr;            // T output
+  float* out_f32 = nullptr;       // f32 output / residual
+  int ldo = 0;
+  int64_t out_group_stride = 0;   // elements between groups (EPI_STORE / GELU)
+  int out_row_off = 0;            // row offset inside a group (conv1 writes after a zero pad row)
+  const float* pos = nullptr;     // EPI_GELU_POS: [rows-in-group][N]
+  // head-split (cross-KV) layout: out[((l2*nslots + slot0+grp)*H + h)*T + t][64]
+  int hs_state = 0, hs_heads = 0, hs_T = 0, hs_nslots = 0, hs_slot0 = 0;
+  // decoder QKV: row metadata + caches [win][slot][head][ctx][64]
+  const int* row_win = nullptr;
+  const int* row_slot = nullptr;
+  const int* row_pos = nullptr;
+  void* kc = nullptr;
+  void* vc = nullptr;
+  int kv_beams = 0, kv_ctx = 0;
+};
+
+template <typename T, int EPI>
+WH_DEV void epilogue_store(const GemmArgs& a, int m, int gi, int ri, int n, float4_t v) {
+  if constexpr (EPI == EPI_STORE || EPI == EPI_STORE_GELU) {
+    if constexpr (EPI == EPI_STORE_GELU) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[j] = gelu_f(v[j]);
+    }
+    T* o = reinterpret_cast<T*>(a.out) + (int64_t)gi * a.out_group_stride + (int64_t)(ri + a.out_row_off) * a.ldo + n;
+    store4(o, v[0], v[1], v[2], v[3]);
+  } else if constexpr (EPI == EPI_RESID) {
+    float* o = a.out_f32 + (int64_t)m * a.ldo + n;
+    float4_t c = load4f(o);
+    c += v;
+    store4(o, c[0], c[1], c[2], c[3]);
+  } else if constexpr (EPI == EPI_GELU_POS) {
+    const float4_t p = load4f(a.pos + (int64_t)ri * a.N + n);
+    float* o = a.out_f32 + (int64_t)m * a.ldo + n;
+    store4(o, gelu_f(v[0]) + p[0], gelu_f(v[1]) + p[1], gelu_f(v[2]) + p[2], gelu_f(v[3]) + p[3]);
+  } else if constexpr (EPI == EPI_HEADSPLIT) {
+    const int l2 = n / a.hs_state, c = n - l2 * a.hs_state, h = c >> 6, d = c & 63;
+    const int64_t idx = ((((int64_t)l2 * a.hs_nslots + a.hs_slot0 + gi) * a.hs_heads + h) * a.hs_T + ri) * 64 + d;
+    store4(reinterpret_cast<T*>(a.out) + idx, v[0], v[1], v[2], v[3]);
+  } else if constexpr (EPI == EPI_QKV_DEC) {
+    const int ns = a.hs_state;
+    if (n < ns) {
+      store4(reinterpret_cast<T*>(a.out) + (int64_t)m * a.ldo + n, v[0], v[1], v[2], v[3]);
+    } else {
+      const int which = n >= 2 * ns;  // 0 = k, 1 = v
+      const int c = n - ns * (1 + which), h = c >> 6, d = c & 63;
+      const int w = a.row_win[m], sl = a.row_slot[m], p = a.row_pos[m];
+      const int64_t idx = ((((int64_t)w * a.kv_beams + sl) * a.hs_heads + h) * a.kv_ctx + p) * 64 + d;
+      T* base = reinterpret_cast<T*>(which ? a.vc : a.kc);
+      store4(base + idx, v[0], v[1], v[2], v[3]);
+    }
+  }
+}
+
+template <typename T>
+int launch_gemm(const GemmArgs& a, int epi, hipStream_t st);
+
+}  // namespace wh

@@ -1,0 +1,253 @@
+// MFMA GEMMs for libwhisper_hip.
+//
+//   Y[m][n] = sum_k X[m][k] * W[n][k]        (W in nn.Linear [out][in] layout)
+//
+// Two kernels:
+//   * k_gemm_tile  — 128x128 output tiles, LDS double buffer, register-staged
+//     global loads; used where M is large (encoder blocks, conv1/conv2 as
+//     overlapping-row im2col views, cross-KV precompute, long prefills).
+//     MFMA-bound: 2*M*N*K flop per call.
+//   * k_gemv_rows  — "skinny" weight-streaming GEMM for M <= 128 rows (decoder
+//     step at W windows x B beams, short prefills, vocab projection).  One
+//     workgroup = 16 output columns x all rows, its 8 waves split K; weights are
+//     streamed from HBM exactly once.  HBM-bound: N*K*sizeof(T) bytes per call.
+//
+// Both use the swapped product D^T = W * X^T so each lane ends with 4
+// consecutive output columns of one row (wide epilogue stores).
+#include "wh_gemm.h"
+
+namespace wh {
+
+// ============================================================ big tile GEMM
+constexpr int TBM = 128, TBN = 128, TKB = 128;  // TKB = bytes of K per tile row
+constexpr int TROW = TKB + 16;                  // padded LDS row stride (bytes): conflict-free b128 reads
+
+template <typename T, int EPI>
+__global__ __launch_bounds__(256, 2) void k_gemm_tile(GemmArgs a) {
+  constexpr int BK = TKB / (int)sizeof(T);  // 64 half / 32 float
+  constexpr int KS = BK / 32;               // k-steps per tile
+  __shared__ __attribute__((aligned(16))) char smem[2][2][TBM * TROW];  // [buf][A/W][rows*stride]
+
+  const int ntn = a.N / TBN;
+  const int ntm = (a.M + TBM - 1) / TBM;
+  const int bid = xcd_remap(blockIdx.x, ntm * ntn);
+  const int tm = bid / ntn, tn = bid % ntn;
+  const int m0 = tm * TBM, n0 = tn * TBN;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wr = wave >> 1, wc = wave & 1;
+  const int r = lane & 15, g = lane >> 4;
+
+  const T* X = reinterpret_cast<const T*>(a.X);
+  const T* W = reinterpret_cast<const T*>(a.W);
+
+  // per-thread global source rows for the 4 chunks of each operand (16 B chunks, 8 per row)
+  const char* xsrc[4];
+  const char* wsrc[4];
+  int lds_off[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int c = tid + 256 * i;
+    const int row = c >> 3, col = c & 7;
+    int m = m0 + row;
+    if (m >= a.M) m = a.M - 1;
+    const int gi = m / a.x_group_rows, ri = m - gi * a.x_group_rows;
+    xsrc[i] = reinterpret_cast<const char*>(X + (int64_t)gi * a.x_group_stride + (int64_t)ri * a.ldx) + col * 16;
+    wsrc[i] = reinterpret_cast<const char*>(W + (int64_t)(n0 + row) * a.K) + col * 16;
+    lds_off[i] = row * TROW + col * 16;
+  }
+  float4_t xs[4], ws[4];
+  auto gload = [&](int kt) {
+    const int kb = kt * TKB;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      xs[i] = *reinterpret_cast<const float4_t*>(xsrc[i] + kb);
+      ws[i] = *reinterpret_cast<const float4_t*>(wsrc[i] + kb);
+    }
+  };
+  auto sstore = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      *reinterpret_cast<float4_t*>(&smem[buf][0][lds_off[i]]) = xs[i];
+      *reinterpret_cast<float4_t*>(&smem[buf][1][lds_off[i]]) = ws[i];
+    }
+  };
+
+  float4_t acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = (float4_t){0.f, 0.f, 0.f, 0.f};
+
+  const int nk = a.K / BK;
+  gload(0);
+  sstore(0);
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    const int buf = kt & 1;
+    if (kt + 1 < nk) gload(kt + 1);
+    const char* As = smem[buf][0];
+    const char* Ws = smem[buf][1];
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      const int koff = (32 * s + 8 * g) * (int)sizeof(T);
+      Frag<T> wf[4], xf[4];
+#pragma unroll
+      for (int ni = 0; ni < 4; ++ni)
+        frag_load(wf[ni], reinterpret_cast<const T*>(Ws + (wc * 64 + ni * 16 + r) * TROW + koff));
+#pragma unroll
+      for (int mi = 0; mi < 4; ++mi)
+        frag_load(xf[mi], reinterpret_cast<const T*>(As + (wr * 64 + mi * 16 + r) * TROW + koff));
+#pragma unroll
+      for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < 4; ++ni) mfma_step(acc[mi][ni], wf[ni], xf[mi]);
+    }
+    if (kt + 1 < nk) sstore(buf ^ 1);
+    __syncthreads();
+  }
+
+  // epilogue: lane holds Y[m = m0+wr*64+mi*16+r][n = n0+wc*64+ni*16+4g .. +3]
+#pragma unroll
+  for (int mi = 0; mi < 4; ++mi) {
+    const int m = m0 + wr * 64 + mi * 16 + r;
+    if (m >= a.M) continue;
+    const int gi = m / a.x_group_rows, ri = m - gi * a.x_group_rows;
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni) {
+      const int n = n0 + wc * 64 + ni * 16 + 4 * g;
+      float4_t v = acc[mi][ni];
+      if (a.bias) {
+        const float4_t b = load4f(a.bias + n);
+        v += b;
+      }
+      epilogue_store<T, EPI>(a, m, gi, ri, n, v);
+    }
+  }
+}
+
+// ============================================================ skinny weight-streaming GEMM
+// grid: (ceil(N/16), ceil(M/(16*MT))), block 512 (8 waves split K in 32-wide steps)
+template <typename T, int MT, int EPI>
+__global__ __launch_bounds__(512) void k_gemv_rows(GemmArgs a) {
+  __shared__ float red[8][MT][64][4];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int r = lane & 15, g = lane >> 4;
+  const int n0 = blockIdx.x * 16;
+  const int mb = blockIdx.y * (16 * MT);
+  const T* X = reinterpret_cast<const T*>(a.X);
+  const T* W = reinterpret_cast<const T*>(a.W);
+
+  int nrow = n0 + r;
+  if (nrow >= a.N) nrow = a.N - 1;
+  const T* wp = W + (int64_t)nrow * a.K + 8 * g;
+  const T* xp[MT];
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt) {
+    int m = mb + mt * 16 + r;
+    if (m >= a.M) m = a.M - 1;
+    xp[mt] = X + (int64_t)m * a.ldx + 8 * g;
+  }
+  float4_t acc[MT];
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt) acc[mt] = (float4_t){0.f, 0.f, 0.f, 0.f};
+
+  const int nsteps = a.K / 32;
+  int s = wave;
+  // unrolled by 4 steps to keep 4 weight loads in flight per lane
+  for (; s + 24 < nsteps; s += 32) {
+    Frag<T> wf[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) frag_load(wf[u], wp + (s + 8 * u) * 32);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) {
+        Frag<T> xf;
+        frag_load(xf, xp[mt] + (s + 8 * u) * 32);
+        mfma_step(acc[mt], wf[u], xf);
+      }
+    }
+  }
+  for (; s < nsteps; s += 8) {
+    Frag<T> wf;
+    frag_load(wf, wp + s * 32);
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+      Frag<T> xf;
+      frag_load(xf, xp[mt] + s * 32);
+      mfma_step(acc[mt], wf, xf);
+    }
+  }
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt)
+    *reinterpret_cast<float4_t*>(&red[wave][mt][lane][0]) = acc[mt];
+  __syncthreads();
+  // 512 threads: thread -> (mt, lane) pairs; fixed-order sum over the 8 waves
+  for (int idx = tid; idx < MT * 64; idx += 512) {
+    const int mt = idx >> 6, ln = idx & 63;
+    float4_t v = *reinterpret_cast<float4_t*>(&red[0][mt][ln][0]);
+#pragma unroll
+    for (int w = 1; w < 8; ++w) v += *reinterpret_cast<float4_t*>(&red[w][mt][ln][0]);
+    const int m = mb + mt * 16 + (ln & 15);
+    const int n = n0 + 4 * (ln >> 4);
+    if (m >= a.M || n >= a.N) continue;
+    if (EPI == EPI_F32_COLS) {  // ragged N (vocab): element-wise store
+      float* o = a.out_f32 + (int64_t)m * a.ldo;
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if (n + j < a.N) o[n + j] = v[j] + (a.bias ? a.bias[n + j] : 0.f);
+      continue;
+    }
+    if (a.bias) v += load4f(a.bias + n);
+    epilogue_store<T, EPI>(a, m, 0, m, n, v);
+  }
+}
+
+// ============================================================ launchers
+template <typename T>
+int launch_gemm(const GemmArgs& a, int epi, hipStream_t st) {
+  if (a.M <= 0) return 0;
+  const bool big = a.M > 128 && (a.N % TBN) == 0 && (a.K % (TKB / (int)sizeof(T))) == 0 && epi != EPI_F32_COLS;
+  if (big) {
+    const int nwg = ((a.M + TBM - 1) / TBM) * (a.N / TBN);
+    switch (epi) {
+#define CASE(E) case E: k_gemm_tile<T, E><<<nwg, 256, 0, st>>>(a); break;
+      CASE(EPI_STORE) CASE(EPI_STORE_GELU) CASE(EPI_RESID) CASE(EPI_GELU_POS) CASE(EPI_HEADSPLIT) CASE(EPI_QKV_DEC)
+#undef CASE
+      default: return -1;
+    }
+  } else {
+    if (a.K % 32) return -2;
+    if (a.x_group_rows != a.M && a.x_group_rows != 0 && a.x_group_rows < a.M) return -3;  // skinny: plain rows only
+    const int mt = (a.M + 15) / 16;
+    const int rows_per = mt >= 8 ? 8 : mt;
+    dim3 grid((a.N + 15) / 16, (a.M + 16 * rows_per - 1) / (16 * rows_per));
+#define LAUNCH(MT_)                                                                             \
+  switch (epi) {                                                                               \
+    case EPI_STORE: k_gemv_rows<T, MT_, EPI_STORE><<<grid, 512, 0, st>>>(a); break;             \
+    case EPI_STORE_GELU: k_gemv_rows<T, MT_, EPI_STORE_GELU><<<grid, 512, 0, st>>>(a); break;   \
+    case EPI_RESID: k_gemv_rows<T, MT_, EPI_RESID><<<grid, 512, 0, st>>>(a); break;             \
+    case EPI_HEADSPLIT: k_gemv_rows<T, MT_, EPI_HEADSPLIT><<<grid, 512, 0, st>>>(a); break;     \
+    case EPI_QKV_DEC: k_gemv_rows<T, MT_, EPI_QKV_DEC><<<grid, 512, 0, st>>>(a); break;         \
+    case EPI_F32_COLS: k_gemv_rows<T, MT_, EPI_F32_COLS><<<grid, 512, 0, st>>>(a); break;       \
+    default: return -1;                                                                        \
+  }
+    switch (rows_per) {
+      case 1: LAUNCH(1) break;
+      case 2: LAUNCH(2) break;
+      case 3: LAUNCH(3) break;
+      case 4: LAUNCH(4) break;
+      case 5: LAUNCH(5) break;
+      case 6: LAUNCH(6) break;
+      case 7: LAUNCH(7) break;
+      default: LAUNCH(8) break;
+    }
+#undef LAUNCH
+  }
+  return 0;
+}
+
+template int launch_gemm<float>(const GemmArgs&, int, hipStream_t);
+template int launch_gemm<half_t>(const GemmArgs&, int, hipStream_t);
+
+}  // namespace wh

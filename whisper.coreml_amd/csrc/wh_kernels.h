@@ -1,0 +1,74 @@
+// Kernel launch declarations for libwhisper_hip.
+#pragma once
+#include "wh_common.h"
+
+namespace wh {
+
+template <typename T>
+void launch_layernorm(const float* x, T* y, const float* g, const float* b, int rows, int n, float eps,
+                      const int* rows_in, hipStream_t st);
+template <typename T>
+void launch_attn_enc(const T* qkv, int ld, int ns, int H, int Tlen, int nwin, int64_t wsi, T* out, int64_t wso,
+                     hipStream_t st);
+template <typename T>
+void launch_self_attn(const T* q, int ldq, const T* kc, const T* vc, const int* rw, const int* rs, const int* rp,
+                      const int* anc, int anc_beams, int nbeam, int H, int ctx, T* out, int ldo, int rows,
+                      hipStream_t st);
+template <typename T>
+void launch_cross_attn(const T* q, int ldq, const T* ck, const T* cv, int Tk, int H, int nsplit, int nwin,
+                       const int* win_row0, const int* win_nrows, const int* win_slot, int64_t win_stride, float* po,
+                       float* pm, float* pl, T* out, int ldo, int rows, float* qk_out, const int* qk_map, int qk_rows,
+                       hipStream_t st);
+template <typename T>
+void launch_embed(const T* E, const T* P, int n, const int* row_tok, int* row_pos, const int* hist,
+                  const int* cur_len, int G, int hctx, int pmax, float* x, int rows, hipStream_t st);
+template <typename T>
+void launch_mel_windows(const float* mel, int64_t ld_mel, int n_mels, const int64_t* seeks, const int* segs, T* melT,
+                        int64_t win_stride, int rows_alloc, int nwin, hipStream_t st);
+template <typename T>
+void launch_zero_rows(T* buf, int64_t ws, int n, int ra, int rb, int nwin, hipStream_t st);
+
+void launch_mel(const float* audio, int64_t n_real, int64_t n_padded, int64_t frame0, int64_t count,
+                const float* filters, int n_mels, float* mel, int64_t ld, unsigned* gmax, hipStream_t st);
+void launch_mel_norm(float* mel, int64_t count, int64_t ld, int n_mels, const unsigned* gmax, const float* ovr,
+                     hipStream_t st);
+
+// ------------------------------------------------------------ decode state (device)
+// Per window slot w (capacity nw) with G rows (beams / samples) each.
+struct DecState {
+  int* hist;         // [nw][G][hctx]   token history (initial tokens + sampled)
+  int* anc;          // [nw][G][ctx]    KV slot of each position (beam reorder by indirection)
+  int* len;          // [nw]            current token count
+  int* sample_begin; // [nw]
+  int* step;         // [nw]            updates done
+  int* done;         // [nw]
+  float* sum_lp;     // [nw][G]
+  int* fin_n;        // [nw]
+  float* fin_score;  // [nw][maxc]
+  int* fin_len;      // [nw][maxc]
+  int* fin_tok;      // [nw][maxc][hctx]
+  float* cand_val;   // [nw*G][KC]
+  int* cand_idx;     // [nw*G][KC]
+  int nw, G, ctx, hctx, maxc;
+};
+
+struct DecOpts {
+  int V, eot, ts_begin, no_ts;       // vocabulary facts
+  int blank[4], n_blank;             // SuppressBlank ids (tokenizer.encode(" ") + eot)
+  const unsigned* suppress;          // bitmask [ceil(V/32)] or null
+  int suppress_blank, timestamps;    // flags
+  int max_initial;                   // max_initial_timestamp index or -1
+  int beam;                          // 1 = beam search, 0 = greedy/sampling
+  int sample_len;                    // max updates
+  int n_ctx;                         // text context (448): stop when len > n_ctx
+  float temperature;                 // > 0: Gumbel-max sampling (greedy decoder)
+  unsigned long long seed;
+};
+
+void launch_logit_rows(const float* logits, int ldl, const DecState& s, const DecOpts& o, int nwin, hipStream_t st);
+void launch_merge(const DecState& s, const DecOpts& o, int nwin, hipStream_t st);
+void launch_no_speech(const float* logits, int ldl, int rows, int V, int no_speech, float* out, hipStream_t st);
+void launch_broadcast_rows(const float* src, int ld_src, const int* src_rows, float* dst, int ld_dst, int G, int nwin,
+                           int V, hipStream_t st);
+
+}  // namespace wh

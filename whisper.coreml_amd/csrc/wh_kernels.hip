@@ -1,0 +1,556 @@
+// Attention, LayerNorm, embedding and log-mel kernels for libwhisper_hip.
+#include "wh_kernels.h"
+
+namespace wh {
+
+// ============================================================ LayerNorm
+// One wave per row: x f32 [rows][n] -> y T [rows][n]; biased variance, two-pass in
+// registers (nn.LayerNorm semantics).  rows_in (nullable) gathers input rows.
+template <typename T>
+__global__ __launch_bounds__(256) void k_layernorm(const float* __restrict__ x, T* __restrict__ y, const float* __restrict__ gamma,
+                                                   const float* __restrict__ beta, int rows, int n, float eps,
+                                                   const int* __restrict__ rows_in) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= rows) return;
+  const int src = rows_in ? rows_in[row] : row;
+  const float* xr = x + (int64_t)src * n;
+  constexpr int MAXV = 8;  // n <= 64*4*8 = 2048
+  float4_t v[MAXV];
+  const int nv = n >> 2;
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < MAXV; ++i) {
+    const int c = lane + 64 * i;
+    if (c < nv) {
+      v[i] = load4f(xr + 4 * c);
+      s += v[i][0] + v[i][1] + v[i][2] + v[i][3];
+    }
+  }
+  const float mean = wave_sum(s) / (float)n;
+  float q = 0.f;
+#pragma unroll
+  for (int i = 0; i < MAXV; ++i) {
+    const int c = lane + 64 * i;
+    if (c < nv) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float d = v[i][j] - mean;
+        q += d * d;
+      }
+    }
+  }
+  const float rstd = rsqrtf(wave_sum(q) / (float)n + eps);
+  T* yr = y + (int64_t)row * n;
+#pragma unroll
+  for (int i = 0; i < MAXV; ++i) {
+    const int c = lane + 64 * i;
+    if (c < nv) {
+      const float4_t gm = load4f(gamma + 4 * c), bt = load4f(beta + 4 * c);
+      store4(yr + 4 * c, (v[i][0] - mean) * rstd * gm[0] + bt[0], (v[i][1] - mean) * rstd * gm[1] + bt[1],
+             (v[i][2] - mean) * rstd * gm[2] + bt[2], (v[i][3] - mean) * rstd * gm[3] + bt[3]);
+    }
+  }
+}
+
+template <typename T>
+void launch_layernorm(const float* x, T* y, const float* g, const float* b, int rows, int n, float eps,
+                      const int* rows_in, hipStream_t st) {
+  if (rows <= 0) return;
+  k_layernorm<T><<<(rows + 3) / 4, 256, 0, st>>>(x, y, g, b, rows, n, eps, rows_in);
+}
+
+// ============================================================ encoder flash attention (non-causal)
+// qkv: [T rows][ld] per window (q at col h*64, k at ns + h*64, v at 2ns + h*64); K is
+// pre-scaled by 1/8 (folded into Wk at load, exact).  out: [T][ns] per window.
+// Block = 4 waves x 16 query rows; 64-key tiles staged in LDS (K row-major, V transposed).
+// S^T = K Q^T and O^T = V^T P^T so each lane owns one query row (see wh_common.h).
+template <typename T>
+__global__ __launch_bounds__(256) void k_attn_enc(const T* __restrict__ qkv, int ld, int ns, int Tlen,
+                                                  int64_t win_stride_in, T* __restrict__ out, int64_t win_stride_out) {
+  constexpr int RS = 64 * (int)sizeof(T) + 16;  // LDS row stride (bytes)
+  __shared__ __attribute__((aligned(16))) char Ks[64 * RS];
+  __shared__ __attribute__((aligned(16))) char Vt[64 * RS];
+  const int h = blockIdx.y, w = blockIdx.z;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int r = lane & 15, g = lane >> 4;
+  const T* base = qkv + (int64_t)w * win_stride_in;
+  const int q0 = blockIdx.x * 64 + wave * 16;
+  int qrow = q0 + r;
+  if (qrow >= Tlen) qrow = Tlen - 1;
+  Frag<T> qf[2];
+  frag_load(qf[0], base + (int64_t)qrow * ld + h * 64 + 8 * g);
+  frag_load(qf[1], base + (int64_t)qrow * ld + h * 64 + 32 + 8 * g);
+
+  float4_t acc_o[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) acc_o[i] = (float4_t){0.f, 0.f, 0.f, 0.f};
+  float m_run = -INFINITY, l_run = 0.f;
+  constexpr float LOG2E = 1.4426950408889634f;
+  constexpr int EPC = 16 / (int)sizeof(T);       // elements per 16 B chunk
+  constexpr int CPR = 64 / EPC;                   // chunks per 64-element row
+  const int nkb = (Tlen + 63) / 64;
+  for (int kb = 0; kb < nkb; ++kb) {
+    // stage: 64 keys x 64 d for K and V
+    for (int c = tid; c < 64 * CPR; c += 256) {
+      const int key = c / CPR, ch = c % CPR;
+      int kr = kb * 64 + key;
+      if (kr >= Tlen) kr = Tlen - 1;
+      const T* src = base + (int64_t)kr * ld + h * 64 + ch * EPC;
+      const float4_t kv = *reinterpret_cast<const float4_t*>(src + ns);
+      *reinterpret_cast<float4_t*>(Ks + key * RS + ch * 16) = kv;
+      const float4_t vv = *reinterpret_cast<const float4_t*>(src + 2 * ns);
+      const T* ve = reinterpret_cast<const T*>(&vv);
+#pragma unroll
+      for (int e = 0; e < EPC; ++e) reinterpret_cast<T*>(Vt + (ch * EPC + e) * RS)[key] = ve[e];
+    }
+    __syncthreads();
+    float4_t sc[4];
+#pragma unroll
+    for (int kt = 0; kt < 4; ++kt) {
+      sc[kt] = (float4_t){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        Frag<T> kf;
+        frag_load(kf, reinterpret_cast<const T*>(Ks + (kt * 16 + r) * RS) + 32 * s + 8 * g);
+        mfma_step(sc[kt], kf, qf[s]);
+      }
+    }
+    // mask ragged last tile; block row max over the 64 keys
+    float mx = -INFINITY;
+#pragma unroll
+    for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int key = kb * 64 + kt * 16 + 4 * g + j;
+        if (key >= Tlen) sc[kt][j] = -INFINITY;
+        mx = fmaxf(mx, sc[kt][j]);
+      }
+    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    const float m_new = fmaxf(m_run, mx);
+    const float alpha = exp2f((m_run - m_new) * LOG2E);
+    float ps = 0.f;
+    Frag<T> pf[2];
+#pragma unroll
+    for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float p = exp2f((sc[kt][j] - m_new) * LOG2E);
+        ps += p;
+        pf[kt >> 1].v[(kt & 1) * 4 + j] = from_f32<T>(p);
+      }
+    ps += __shfl_xor(ps, 16, 64);
+    ps += __shfl_xor(ps, 32, 64);
+    l_run = l_run * alpha + ps;
+    m_run = m_new;
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) {
+      acc_o[dt] *= alpha;
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        Frag<T> vf;
+        const T* vrow = reinterpret_cast<const T*>(Vt + (dt * 16 + r) * RS);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          vf.v[j] = vrow[32 * s + 4 * g + j];
+          vf.v[4 + j] = vrow[32 * s + 16 + 4 * g + j];
+        }
+        mfma_step(acc_o[dt], vf, pf[s]);
+      }
+    }
+    __syncthreads();
+  }
+  const int q = q0 + r;
+  if (q < Tlen) {
+    const float inv = 1.f / l_run;
+    T* o = out + (int64_t)w * win_stride_out + (int64_t)q * ns + h * 64;
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt)
+      store4(o + dt * 16 + 4 * g, acc_o[dt][0] * inv, acc_o[dt][1] * inv, acc_o[dt][2] * inv, acc_o[dt][3] * inv);
+  }
+}
+
+template <typename T>
+void launch_attn_enc(const T* qkv, int ld, int ns, int H, int Tlen, int nwin, int64_t wsi, T* out, int64_t wso,
+                     hipStream_t st) {
+  dim3 grid((Tlen + 63) / 64, H, nwin);
+  k_attn_enc<T><<<grid, 256, 0, st>>>(qkv, ld, ns, Tlen, wsi, out, wso);
+}
+
+// ============================================================ decoder self-attention
+// One wave per (row, head).  Keys = positions 0..pos of the row's sequence; position
+// p < pos lives in beam slot anc[win][slot][p] (beam reorder by index indirection,
+// no KV copies), position pos in the row's own slot.  Cache: [win][slot][head][ctx][64].
+template <typename T>
+__global__ __launch_bounds__(64) void k_self_attn(const T* __restrict__ q, int ldq, const T* __restrict__ kc,
+                                                  const T* __restrict__ vc, const int* __restrict__ row_win,
+                                                  const int* __restrict__ row_slot, const int* __restrict__ row_pos,
+                                                  const int* __restrict__ anc, int anc_beams, int nbeam, int H,
+                                                  int ctx, T* __restrict__ out, int ldo) {
+  __shared__ float sc[512];
+  __shared__ int slot_of[512];
+  const int row = blockIdx.x, h = blockIdx.y, lane = threadIdx.x;
+  const int w = row_win[row], sl = row_slot[row], pos = row_pos[row];
+  const int* an = anc + ((int64_t)w * anc_beams + sl) * ctx;
+  float qv[64];
+  {
+    const T* qr = q + (int64_t)row * ldq + h * 64;
+#pragma unroll
+    for (int c = 0; c < 64; c += 4) {
+      const float4_t t = load4f(qr + c);
+      qv[c] = t[0]; qv[c + 1] = t[1]; qv[c + 2] = t[2]; qv[c + 3] = t[3];
+    }
+  }
+  const int64_t head_stride = (int64_t)ctx * 64;
+  auto kv_off = [&](int slot, int p) -> int64_t {
+    return ((((int64_t)w * nbeam + slot) * H + h) * head_stride) + (int64_t)p * 64;
+  };
+  float mx = -INFINITY;
+  for (int p = lane; p <= pos; p += 64) {
+    const int slot = (p == pos) ? sl : an[p];
+    slot_of[p] = slot;
+    const T* kr = kc + kv_off(slot, p);
+    float s = 0.f;
+#pragma unroll
+    for (int c = 0; c < 64; c += 4) {
+      const float4_t t = load4f(kr + c);
+      s += qv[c] * t[0] + qv[c + 1] * t[1] + qv[c + 2] * t[2] + qv[c + 3] * t[3];
+    }
+    sc[p] = s;
+    mx = fmaxf(mx, s);
+  }
+  mx = wave_max(mx);
+  float sum = 0.f;
+  for (int p = lane; p <= pos; p += 64) {
+    const float e = __expf(sc[p] - mx);
+    sc[p] = e;
+    sum += e;
+  }
+  sum = wave_sum(sum);
+  __syncthreads();
+  // lane = output dim d
+  float o = 0.f;
+  int p = 0;
+  for (; p + 4 <= pos + 1; p += 4) {
+    const float v0 = to_f32(vc[kv_off(slot_of[p], p) + lane]);
+    const float v1 = to_f32(vc[kv_off(slot_of[p + 1], p + 1) + lane]);
+    const float v2 = to_f32(vc[kv_off(slot_of[p + 2], p + 2) + lane]);
+    const float v3 = to_f32(vc[kv_off(slot_of[p + 3], p + 3) + lane]);
+    o += sc[p] * v0 + sc[p + 1] * v1 + sc[p + 2] * v2 + sc[p + 3] * v3;
+  }
+  for (; p <= pos; ++p) o += sc[p] * to_f32(vc[kv_off(slot_of[p], p) + lane]);
+  out[(int64_t)row * ldo + h * 64 + lane] = from_f32<T>(o / sum);
+}
+
+template <typename T>
+void launch_self_attn(const T* q, int ldq, const T* kc, const T* vc, const int* rw, const int* rs, const int* rp,
+                      const int* anc, int anc_beams, int nbeam, int H, int ctx, T* out, int ldo, int rows,
+                      hipStream_t st) {
+  if (rows <= 0) return;
+  k_self_attn<T><<<dim3(rows, H), 64, 0, st>>>(q, ldq, kc, vc, rw, rs, rp, anc, anc_beams, nbeam, H, ctx, out, ldo);
+}
+
+// ============================================================ decoder cross-attention (split-K flash decoding)
+// grid (windows, H, nsplit); block 256.  All rows of a window (beams, or prefill
+// tokens) share one pass over that split's keys: K/V are read from HBM once per
+// window per step.  ck/cv: [win][head][Tk][64] for this layer.
+// Partials: po[row][h][split][64], pm/pl[row][h][split].
+// If qk_map != null the raw scores q.k of alignment heads are also written
+// (word timestamps, decoder.py:306-308): qk_out[(qk_map[h] * qk_rows + row) * Tk + key]
+// for heads with qk_map[h] >= 0.
+constexpr int XA_MAXR = 16;
+template <typename T>
+__global__ __launch_bounds__(256) void k_cross_attn(const T* __restrict__ q, int ldq, const T* __restrict__ ck,
+                                                    const T* __restrict__ cv, int Tk, int H, int nsplit,
+                                                    const int* __restrict__ win_row0, const int* __restrict__ win_nrows,
+                                                    const int* __restrict__ win_slot, int64_t win_stride,
+                                                    float* __restrict__ po, float* __restrict__ pm, float* __restrict__ pl,
+                                                    float* qk_out, const int* qk_map, int qk_rows) {
+  constexpr int CH = 192;  // max keys per split
+  __shared__ float qs[XA_MAXR][64];
+  __shared__ float sc[XA_MAXR][CH + 1];
+  __shared__ T vs[CH][64];
+  const int wi = blockIdx.x, h = blockIdx.y, sp = blockIdx.z;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int row0 = win_row0[wi], nrows = win_nrows[wi];
+  const int chunk = (Tk + nsplit - 1) / nsplit;
+  const int k0 = sp * chunk, k1 = min(Tk, k0 + chunk);
+  const int qslot = qk_map ? qk_map[h] : -1;
+  const int nk = k1 - k0;
+  const T* kb = ck + (int64_t)win_slot[wi] * win_stride + (int64_t)h * Tk * 64;
+  const T* vb = cv + (int64_t)win_slot[wi] * win_stride + (int64_t)h * Tk * 64;
+  // stage V chunk
+  for (int c = tid; c < nk * 64 / 8; c += 256) {
+    const int key = c >> 3, part = c & 7;
+    const T* src = vb + (int64_t)(k0 + key) * 64 + part * 8;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) vs[key][part * 8 + e] = src[e];
+  }
+  // K row for this thread's key held in registers
+  float kr[64];
+  const bool has_key = tid < nk;
+  if (has_key) {
+    const T* src = kb + (int64_t)(k0 + tid) * 64;
+#pragma unroll
+    for (int c = 0; c < 64; c += 4) {
+      const float4_t t = load4f(src + c);
+      kr[c] = t[0]; kr[c + 1] = t[1]; kr[c + 2] = t[2]; kr[c + 3] = t[3];
+    }
+  }
+  for (int rb = 0; rb < nrows; rb += XA_MAXR) {
+    const int nr = min(XA_MAXR, nrows - rb);
+    __syncthreads();
+    for (int c = tid; c < nr * 64; c += 256) {
+      const int i = c >> 6, d = c & 63;
+      qs[i][d] = to_f32(q[(int64_t)(row0 + rb + i) * ldq + h * 64 + d]);
+    }
+    __syncthreads();
+    if (has_key) {
+      for (int i = 0; i < nr; ++i) {
+        float s = 0.f;
+#pragma unroll
+        for (int d = 0; d < 64; ++d) s += qs[i][d] * kr[d];
+        sc[i][tid] = s;
+        if (qslot >= 0) qk_out[((int64_t)qslot * qk_rows + row0 + rb + i) * Tk + k0 + tid] = s;
+      }
+    }
+    __syncthreads();
+    // per-row max / exp / sum: wave handles rows wave, wave+4, ...
+    for (int i = wave; i < nr; i += 4) {
+      float mx = -INFINITY;
+      for (int k = lane; k < nk; k += 64) mx = fmaxf(mx, sc[i][k]);
+      mx = wave_max(mx);
+      float sm = 0.f;
+      for (int k = lane; k < nk; k += 64) {
+        const float e = __expf(sc[i][k] - mx);
+        sc[i][k] = e;
+        sm += e;
+      }
+      sm = wave_sum(sm);
+      if (lane == 0) {
+        const int64_t pi = ((int64_t)(row0 + rb + i) * H + h) * nsplit + sp;
+        pm[pi] = mx;
+        pl[pi] = sm;
+      }
+    }
+    __syncthreads();
+    for (int i = wave; i < nr; i += 4) {
+      float o = 0.f;
+      for (int k = 0; k < nk; ++k) o += sc[i][k] * to_f32(vs[k][lane]);
+      po[(((int64_t)(row0 + rb + i) * H + h) * nsplit + sp) * 64 + lane] = o;
+    }
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(64) void k_cross_combine(const float* __restrict__ po, const float* __restrict__ pm,
+                                                      const float* __restrict__ pl, int H, int nsplit,
+                                                      T* __restrict__ out, int ldo) {
+  const int row = blockIdx.x, h = blockIdx.y, lane = threadIdx.x;
+  const int64_t b = ((int64_t)row * H + h) * nsplit;
+  float M = -INFINITY;
+  for (int s = 0; s < nsplit; ++s) M = fmaxf(M, pm[b + s]);
+  float num = 0.f, den = 0.f;
+  for (int s = 0; s < nsplit; ++s) {
+    const float f = __expf(pm[b + s] - M);
+    num += f * po[(b + s) * 64 + lane];
+    den += f * pl[b + s];
+  }
+  out[(int64_t)row * ldo + h * 64 + lane] = from_f32<T>(num / den);
+}
+
+template <typename T>
+void launch_cross_attn(const T* q, int ldq, const T* ck, const T* cv, int Tk, int H, int nsplit, int nwin,
+                       const int* win_row0, const int* win_nrows, const int* win_slot, int64_t win_stride, float* po,
+                       float* pm, float* pl, T* out, int ldo, int rows, float* qk_out, const int* qk_map, int qk_rows,
+                       hipStream_t st) {
+  if (rows <= 0) return;
+  k_cross_attn<T><<<dim3(nwin, H, nsplit), 256, 0, st>>>(q, ldq, ck, cv, Tk, H, nsplit, win_row0, win_nrows, win_slot,
+                                                         win_stride, po, pm, pl, qk_out, qk_map, qk_rows);
+  k_cross_combine<T><<<dim3(rows, H), 64, 0, st>>>(po, pm, pl, H, nsplit, out, ldo);
+}
+
+// ============================================================ embedding
+// x[r] = E[tok] + P[pos] (fp32 residual).  State mode (hist != null): row r = w*G + b,
+// tok = hist[(w*G+b)*hctx + len[w]-1], pos = len[w]-1, and row_pos[r] is written.
+template <typename T>
+__global__ __launch_bounds__(256) void k_embed(const T* __restrict__ E, const T* __restrict__ P, int n,
+                                               const int* __restrict__ row_tok, int* __restrict__ row_pos,
+                                               const int* __restrict__ hist, const int* __restrict__ cur_len, int G,
+                                               int hctx, int pmax, float* __restrict__ x) {
+  const int r = blockIdx.x;
+  int tok, pos;
+  if (hist) {
+    const int w = r / G;
+    pos = min(cur_len[w] - 1, pmax);  // finished windows past n_ctx keep recomputing a valid row
+    tok = hist[(int64_t)r * hctx + pos];
+    if (threadIdx.x == 0) row_pos[r] = pos;
+  } else {
+    tok = row_tok[r];
+    pos = row_pos[r];
+  }
+  for (int c = threadIdx.x; c < n; c += 256)
+    x[(int64_t)r * n + c] = to_f32(E[(int64_t)tok * n + c]) + to_f32(P[(int64_t)pos * n + c]);
+}
+
+template <typename T>
+void launch_embed(const T* E, const T* P, int n, const int* row_tok, int* row_pos, const int* hist,
+                  const int* cur_len, int G, int hctx, int pmax, float* x, int rows, hipStream_t st) {
+  if (rows <= 0) return;
+  k_embed<T><<<rows, 256, 0, st>>>(E, P, n, row_tok, row_pos, hist, cur_len, G, hctx, pmax, x);
+}
+
+// ============================================================ encoder input prep
+// mel [n_mels][ld_mel] (normalized, f32) -> melT[w][1 + t][n_mels] (T), zero rows at
+// t = -1 and t >= seg (pad_or_trim), slice [seek, seek+seg) of the full mel.
+template <typename T>
+__global__ void k_mel_windows(const float* __restrict__ mel, int64_t ld_mel, int n_mels, const int64_t* __restrict__ seeks,
+                              const int* __restrict__ segs, T* __restrict__ melT, int64_t win_stride, int rows_alloc) {
+  const int w = blockIdx.y;
+  const int64_t seek = seeks[w];
+  const int seg = segs[w];
+  const int total = rows_alloc * n_mels;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+    const int rr = i / n_mels, c = i - rr * n_mels;
+    const int t = rr - 1;
+    float v = 0.f;
+    if (t >= 0 && t < 3000 && t < seg) v = mel[(int64_t)c * ld_mel + seek + t];
+    melT[(int64_t)w * win_stride + i] = from_f32<T>(v);
+  }
+}
+
+template <typename T>
+void launch_mel_windows(const float* mel, int64_t ld_mel, int n_mels, const int64_t* seeks, const int* segs, T* melT,
+                        int64_t win_stride, int rows_alloc, int nwin, hipStream_t st) {
+  k_mel_windows<T><<<dim3(64, nwin), 256, 0, st>>>(mel, ld_mel, n_mels, seeks, segs, melT, win_stride, rows_alloc);
+}
+
+// zero pad rows around the conv1 output (rows 0 and 3001 of each window)
+template <typename T>
+__global__ void k_zero_rows(T* buf, int64_t win_stride, int n, int row_a, int row_b) {
+  const int w = blockIdx.x;
+  for (int c = threadIdx.x; c < n; c += blockDim.x) {
+    buf[(int64_t)w * win_stride + (int64_t)row_a * n + c] = from_f32<T>(0.f);
+    buf[(int64_t)w * win_stride + (int64_t)row_b * n + c] = from_f32<T>(0.f);
+  }
+}
+template <typename T>
+void launch_zero_rows(T* buf, int64_t ws, int n, int ra, int rb, int nwin, hipStream_t st) {
+  k_zero_rows<T><<<nwin, 256, 0, st>>>(buf, ws, n, ra, rb);
+}
+
+// ============================================================ log-mel spectrogram
+// audio.py:110-157.  Frame f is centred at f*160 with reflect padding; 400-point
+// periodic Hann; |DFT|^2 for bins 0..200 (direct DFT, fp32, twiddles from a
+// 400-entry table); mel = filters @ power; log10(max(mel, 1e-10)).  The global max
+// is accumulated with an ordered-uint atomicMax; k_mel_norm applies max(x, gmax-8)
+// and (x+4)/4.  16 frames per block.
+constexpr int MEL_FB = 16;
+__global__ __launch_bounds__(256) void k_mel_frames(const float* __restrict__ audio, int64_t n_real, int64_t n_audio, int64_t nframes,
+                                                    int64_t frame0, const float* __restrict__ filters, int n_mels,
+                                                    float* __restrict__ mel, int64_t ld_mel, unsigned* gmax) {
+  __shared__ float xs[MEL_FB][400];
+  __shared__ float cs[400], sn[400];
+  __shared__ float pw[MEL_FB][201];
+  const int tid = threadIdx.x;
+  const int64_t f0 = frame0 + (int64_t)blockIdx.x * MEL_FB;
+  for (int i = tid; i < 400; i += 256) {
+    float s, c;
+    sincospif((float)i / 200.0f, &s, &c);  // angle 2*pi*i/400
+    cs[i] = c;
+    sn[i] = s;
+  }
+  for (int i = tid; i < MEL_FB * 400; i += 256) {
+    const int fi = i / 400, j = i - fi * 400;
+    const int64_t f = f0 + fi;
+    float v = 0.f;
+    if (f < nframes) {
+      int64_t idx = f * 160 + j - 200;
+      if (idx < 0) idx = -idx;
+      if (idx >= n_audio) idx = 2 * (n_audio - 1) - idx;
+      v = idx < n_real ? audio[idx] : 0.f;  // right zero-padding is virtual
+    }
+    xs[fi][j] = v;
+  }
+  __syncthreads();
+  for (int i = tid; i < MEL_FB * 400; i += 256) {
+    const int fi = i / 400, j = i - fi * 400;
+    // periodic hann: 0.5 - 0.5 cos(2 pi j / 400)
+    xs[fi][j] *= 0.5f - 0.5f * cs[j];
+  }
+  __syncthreads();
+  for (int i = tid; i < MEL_FB * 201; i += 256) {
+    const int fi = i / 201, k = i - fi * 201;
+    float re = 0.f, im = 0.f;
+    int ph = 0;
+    for (int j = 0; j < 400; ++j) {
+      const float x = xs[fi][j];
+      re += x * cs[ph];
+      im -= x * sn[ph];
+      ph += k;
+      if (ph >= 400) ph -= 400;
+    }
+    pw[fi][k] = re * re + im * im;
+  }
+  __syncthreads();
+  float lmax = -INFINITY;
+  for (int i = tid; i < MEL_FB * n_mels; i += 256) {
+    const int fi = i / n_mels, m = i - fi * n_mels;
+    const int64_t f = f0 + fi;
+    if (f >= nframes) continue;
+    const float* fr = filters + m * 201;
+    float s = 0.f;
+    for (int k = 0; k < 201; ++k) s += fr[k] * pw[fi][k];
+    const float lv = log10f(fmaxf(s, 1e-10f));
+    mel[(int64_t)m * ld_mel + (f - frame0)] = lv;
+    lmax = fmaxf(lmax, lv);
+  }
+  lmax = wave_max(lmax);
+  if ((tid & 63) == 0) atomicMax(gmax, f2ord(lmax));
+}
+
+__global__ void k_mel_norm(float* mel, int64_t count_per_row, int64_t ld, int n_mels, const unsigned* gmax,
+                           const float* gmax_override) {
+  const float mx = gmax_override ? *gmax_override : ord2f(*gmax);
+  const float floor_v = mx - 8.0f;
+  const int64_t total = (int64_t)n_mels * count_per_row;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int m = (int)(i / count_per_row);
+    const int64_t f = i - (int64_t)m * count_per_row;
+    float* p = mel + (int64_t)m * ld + f;
+    *p = (fmaxf(*p, floor_v) + 4.0f) * 0.25f;
+  }
+}
+
+void launch_mel(const float* audio, int64_t n_real, int64_t n_padded, int64_t frame0, int64_t count,
+                const float* filters, int n_mels, float* mel, int64_t ld, unsigned* gmax, hipStream_t st) {
+  const int64_t nb = (count + MEL_FB - 1) / MEL_FB;
+  if (nb > 0)
+    k_mel_frames<<<(unsigned)nb, 256, 0, st>>>(audio, n_real, n_padded, frame0 + count, frame0, filters, n_mels, mel, ld, gmax);
+}
+void launch_mel_norm(float* mel, int64_t count, int64_t ld, int n_mels, const unsigned* gmax, const float* ovr,
+                     hipStream_t st) {
+  k_mel_norm<<<1024, 256, 0, st>>>(mel, count, ld, n_mels, gmax, ovr);
+}
+
+// explicit instantiations
+#define INST(T)                                                                                                     \
+  template void launch_layernorm<T>(const float*, T*, const float*, const float*, int, int, float, const int*,     \
+                                    hipStream_t);                                                                   \
+  template void launch_attn_enc<T>(const T*, int, int, int, int, int, int64_t, T*, int64_t, hipStream_t);          \
+  template void launch_self_attn<T>(const T*, int, const T*, const T*, const int*, const int*, const int*,         \
+                                    const int*, int, int, int, int, T*, int, int, hipStream_t);                          \
+  template void launch_cross_attn<T>(const T*, int, const T*, const T*, int, int, int, int, const int*, const int*, \
+                                     const int*, int64_t, float*, float*, float*, T*, int, int, float*,             \
+                                     const int*, int, hipStream_t);                                                         \
+  template void launch_embed<T>(const T*, const T*, int, const int*, int*, const int*, const int*, int, int, int,  \
+                                float*, int, hipStream_t);                                                          \
+  template void launch_mel_windows<T>(const float*, int64_t, int, const int64_t*, const int*, T*, int64_t, int, int, \
+                                      hipStream_t);                                                                 \
+  template void launch_zero_rows<T>(T*, int64_t, int, int, int, int, hipStream_t);
+INST(float)
+INST(half_t)
+#undef INST
+
+}  // namespace wh

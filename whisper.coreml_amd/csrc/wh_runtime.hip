@@ -1,0 +1,1031 @@
+// libwhisper_hip runtime: context, weights, buffers, stage drivers and the C ABI
+// declared in include/whisper_hip.h.  The reference counterpart is the
+// Objective-C++ CoreML runner coreml/coreml.mm:18-463 (process-global state, one
+// model per process, void returns); here everything lives in a context object,
+// every entry point returns a status, and all stage data stays in HBM.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <set>
+#include <string>
+#include <vector>
+
+#include "whisper_hip.h"
+#include "wh_gemm.h"
+#include "wh_kernels.h"
+
+using namespace wh;
+
+static thread_local std::string g_err;
+static int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+
+#define HIPCHK(expr)                                                                                  \
+  do {                                                                                                \
+    hipError_t e_ = (expr);                                                                           \
+    if (e_ != hipSuccess) return fail(-100, std::string(#expr) + ": " + hipGetErrorString(e_));       \
+  } while (0)
+
+#define TRY(expr)                  \
+  do {                             \
+    int rc_ = (expr);              \
+    if (rc_ != 0) return rc_;      \
+  } while (0)
+
+namespace {
+
+constexpr int CTX = 448;          // text positions (decoder.py:243, decoding.py:173)
+constexpr int HCTX = CTX + 1;     // history capacity (tokens.shape[-1] may reach n_ctx + 1)
+constexpr int NSPLIT = 8;         // cross-attention key splits (1500 / 8 = 188 keys)
+constexpr int ENC_CHUNK = 16;     // encoder windows per pass
+constexpr int PRE_ROWS = 1024;    // prefill rows per pass
+constexpr int MROWS = 3008;       // melT rows per window (1 pad + 3000 + slack for padded conv1 K)
+constexpr int H1ROWS = 3002;      // conv1 output rows per window (zero rows 0 and 3001)
+constexpr int KC = 9;
+
+struct Arena {
+  char* base = nullptr;
+  size_t cap = 0, off = 0;
+  void* take(size_t bytes) {
+    off = (off + 255) & ~size_t(255);
+    void* p = base + off;
+    off += bytes;
+    return off <= cap ? p : nullptr;
+  }
+};
+
+template <typename T>
+struct EncLayer {
+  float *ln1_g, *ln1_b, *bqkv, *bo, *ln2_g, *ln2_b, *b1, *b2;
+  T *wqkv, *wo, *w1, *w2;
+};
+template <typename T>
+struct DecLayer {
+  float *ln1_g, *ln1_b, *bqkv, *bo, *lnx_g, *lnx_b, *bqx, *box, *ln2_g, *ln2_b, *b1, *b2;
+  T *wqkv, *wo, *wqx, *wox, *w1, *w2;
+};
+
+struct Timer {
+  hipEvent_t a = nullptr, b = nullptr;
+  void create() { hipEventCreate(&a); hipEventCreate(&b); }
+  ~Timer() {
+    if (a) hipEventDestroy(a);
+    if (b) hipEventDestroy(b);
+  }
+};
+
+}  // namespace
+
+struct wh_ctx {
+  virtual ~wh_ctx() {}
+  virtual int load(const std::string& name, const float* data, const int64_t* shape, int ndim) = 0;
+  virtual int finalize() = 0;
+  virtual int log_mel(const float* audio, int64_t n, int64_t pad, int n_mels, int normalize, int64_t* nf) = 0;
+  virtual int mel_max(float* g) = 0;
+  virtual int mel_normalize(float g) = 0;
+  virtual int mel_read(float* out, int64_t f0, int64_t nf) = 0;
+  virtual int mel_write(const float* mel, int64_t nf) = 0;
+  virtual int encode(int n_win, const int64_t* seeks, const int* segs) = 0;
+  virtual int read_xa(int slot, float* out) = 0;
+  virtual int read_ckv(int slot, int layer, float* k, float* v) = 0;
+  virtual int decode_begin(int n_win, const wh_decode_opts* o, const int* init, const int* n_init, int max_init,
+                           const int* sot_index) = 0;
+  virtual int decode_steps(int max_steps, int* n_done) = 0;
+  virtual int decode_read(int slot, int* tokens, float* slp, int* len, int* fin_n, int* fin_tok, int* fin_len,
+                          float* fin_score, float* nsp) = 0;
+  virtual int prefill_logits(int slot, const int* tokens, int n, float* logits, const int* ah, int na, float* aqk) = 0;
+  virtual int time_stage(int what, int iters, double* ms) = 0;
+  double stats[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  int maxc = 5;
+  int maxc_stride = 1;
+  int device = 0;
+};
+
+namespace {
+
+template <typename T>
+struct Ctx : public wh_ctx {
+  wh_dims d;
+  int ns, nh, La, Ld, V, nm, K1p;
+  int Wcap, Gcap;
+  hipStream_t st = nullptr;
+  Arena wa;  // weights
+  Arena aa;  // activations / state
+  void* wbase = nullptr;
+  void* abase = nullptr;
+  std::set<std::string> loaded;
+  size_t expected = 0;
+  bool finalized = false;
+
+  // weights
+  T *conv1_w, *conv2_w, *E, *Pdec, *ckv_w;
+  float *conv1_b, *conv2_b, *pos_enc, *lnp_g, *lnp_b, *ln_g, *ln_b, *ckv_b;
+  std::vector<EncLayer<T>> enc;
+  std::vector<DecLayer<T>> dec;
+
+  // mel
+  float* d_audio = nullptr;
+  size_t audio_cap = 0;
+  float* d_mel = nullptr;
+  size_t mel_cap = 0;
+  int64_t mel_frames = 0;
+  int mel_nm = 0;
+  unsigned* d_gmax = nullptr;
+  float* d_gmax_f = nullptr;
+  std::map<int, float*> d_filters;
+
+  // encoder buffers
+  T *melT, *h1, *xn_e, *qkv_e, *att_e, *hm_e, *xa, *ckv;
+  float* x_e;
+  int64_t* d_seeks;
+  int* d_segs;
+  // self KV per layer
+  std::vector<T*> kc, vc;
+  // decoder buffers
+  int RD;
+  float *x_d, *po, *pm, *pl, *logits, *logits2, *nsp;
+  T *xn_d, *q_d, *att_d, *hm_d;
+  int *row_tok, *row_pos, *row_win, *row_slot, *win_row0, *win_nrows, *win_slot, *rows_in, *src_rows;
+  int *st_row_win, *st_row_slot, *st_win_row0, *st_win_nrows, *st_win_slot;
+  int* qk_map;  // [Ld][nh]
+  unsigned* suppress;
+  DecState S;
+  DecOpts O;
+  int cur_nwin = 0, cur_G = 1;
+  // graph cache
+  hipGraph_t graph = nullptr;
+  hipGraphExec_t gexec = nullptr;
+  std::vector<char> graph_key;
+  int* h_done = nullptr;
+
+  Timer tm;
+
+  ~Ctx() override {
+    if (gexec) hipGraphExecDestroy(gexec);
+    if (graph) hipGraphDestroy(graph);
+    if (st) hipStreamDestroy(st);
+    if (wbase) hipFree(wbase);
+    if (abase) hipFree(abase);
+    if (d_audio) hipFree(d_audio);
+    if (d_mel) hipFree(d_mel);
+    for (auto& kv : d_filters) hipFree(kv.second);
+    if (h_done) hipHostFree(h_done);
+  }
+
+  int init(int device_, const wh_dims& dims, int Wcap_, int Gcap_) {
+    device = device_;
+    d = dims;
+    ns = d.n_text_state;
+    nh = d.n_text_head;
+    La = d.n_audio_layer;
+    Ld = d.n_text_layer;
+    V = d.n_vocab;
+    nm = d.n_mels;
+    if (d.n_audio_state != ns || d.n_audio_head != nh) return fail(-2, "audio/text state or head mismatch unsupported");
+    if (ns != nh * 64) return fail(-2, "head dim must be 64 (decoder.py:62-64)");
+    if (d.n_audio_ctx != 1500 || d.n_text_ctx != CTX) return fail(-2, "n_audio_ctx must be 1500, n_text_ctx 448");
+    if (ns % 128 || ns > 2048) return fail(-2, "n_state must be a multiple of 128 and <= 2048");
+    if (V > 57344) return fail(-2, "n_vocab too large");
+    Wcap = Wcap_;
+    Gcap = Gcap_;
+    if (Wcap < 1 || Gcap < 1 || Gcap > 8) return fail(-2, "bad max_windows / max_group");
+    const int kb = 128 / (int)sizeof(T);
+    K1p = ((3 * nm + kb - 1) / kb) * kb;
+    HIPCHK(hipSetDevice(device));
+    HIPCHK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+    tm.create();
+    HIPCHK(hipHostMalloc((void**)&h_done, sizeof(int) * Wcap));
+    // ---------------- weights
+    const size_t n = ns;
+    size_t wb = 0;
+    auto add = [&](size_t elems, size_t esz) { wb += ((elems * esz + 255) & ~size_t(255)) + 256; };
+    add(n * K1p, sizeof(T)); add(n, 4); add(n * 3 * n, sizeof(T)); add(n, 4); add(1500 * n, 4);
+    for (int l = 0; l < La; ++l) {
+      add(n, 4); add(n, 4); add(3 * n * n, sizeof(T)); add(3 * n, 4); add(n * n, sizeof(T)); add(n, 4);
+      add(n, 4); add(n, 4); add(4 * n * n, sizeof(T)); add(4 * n, 4); add(4 * n * n, sizeof(T)); add(n, 4);
+    }
+    add(n, 4); add(n, 4);
+    add((size_t)V * n, sizeof(T)); add(CTX * n, sizeof(T));
+    for (int l = 0; l < Ld; ++l) {
+      add(n, 4); add(n, 4); add(3 * n * n, sizeof(T)); add(3 * n, 4); add(n * n, sizeof(T)); add(n, 4);
+      add(n, 4); add(n, 4); add(n * n, sizeof(T)); add(n, 4); add(n * n, sizeof(T)); add(n, 4);
+      add(n, 4); add(n, 4); add(4 * n * n, sizeof(T)); add(4 * n, 4); add(4 * n * n, sizeof(T)); add(n, 4);
+    }
+    add(n, 4); add(n, 4);
+    add(2 * Ld * n * n, sizeof(T)); add(2 * Ld * n, 4);
+    HIPCHK(hipMalloc(&wbase, wb));
+    HIPCHK(hipMemset(wbase, 0, wb));
+    wa.base = (char*)wbase;
+    wa.cap = wb;
+    auto tk = [&](size_t elems) { return (T*)wa.take(elems * sizeof(T)); };
+    auto fk = [&](size_t elems) { return (float*)wa.take(elems * 4); };
+    conv1_w = tk(n * K1p); conv1_b = fk(n); conv2_w = tk(n * 3 * n); conv2_b = fk(n); pos_enc = fk(1500 * n);
+    enc.resize(La);
+    for (auto& e : enc) {
+      e.ln1_g = fk(n); e.ln1_b = fk(n); e.wqkv = tk(3 * n * n); e.bqkv = fk(3 * n); e.wo = tk(n * n); e.bo = fk(n);
+      e.ln2_g = fk(n); e.ln2_b = fk(n); e.w1 = tk(4 * n * n); e.b1 = fk(4 * n); e.w2 = tk(4 * n * n); e.b2 = fk(n);
+    }
+    lnp_g = fk(n); lnp_b = fk(n);
+    E = tk((size_t)V * n); Pdec = tk(CTX * n);
+    dec.resize(Ld);
+    for (auto& e : dec) {
+      e.ln1_g = fk(n); e.ln1_b = fk(n); e.wqkv = tk(3 * n * n); e.bqkv = fk(3 * n); e.wo = tk(n * n); e.bo = fk(n);
+      e.lnx_g = fk(n); e.lnx_b = fk(n); e.wqx = tk(n * n); e.bqx = fk(n); e.wox = tk(n * n); e.box = fk(n);
+      e.ln2_g = fk(n); e.ln2_b = fk(n); e.w1 = tk(4 * n * n); e.b1 = fk(4 * n); e.w2 = tk(4 * n * n); e.b2 = fk(n);
+    }
+    ln_g = fk(n); ln_b = fk(n);
+    ckv_w = tk(2 * Ld * n * n); ckv_b = fk(2 * Ld * n);
+    if (!ckv_b) return fail(-3, "weight arena overflow");
+    expected = 5 + La * 15 + 2 + 2 + Ld * 24 + 2;
+    // ---------------- activations
+    const int WE = std::min(Wcap, ENC_CHUNK);
+    RD = std::max(Wcap * Gcap, PRE_ROWS);
+    const int LR = std::max(Wcap * Gcap, 2 * Wcap);
+    size_t ab = 0;
+    auto addA = [&](size_t bytes) { ab += ((bytes + 255) & ~size_t(255)) + 256; };
+    addA((size_t)WE * MROWS * nm * sizeof(T)); addA((size_t)WE * H1ROWS * n * sizeof(T));
+    addA((size_t)WE * 1500 * n * 4); addA((size_t)WE * 1500 * n * sizeof(T)); addA((size_t)WE * 1500 * 3 * n * sizeof(T));
+    addA((size_t)WE * 1500 * n * sizeof(T)); addA((size_t)WE * 1500 * 4 * n * sizeof(T));
+    addA((size_t)Wcap * 1500 * n * sizeof(T));
+    addA((size_t)2 * Ld * Wcap * 1500 * n * sizeof(T));
+    for (int l = 0; l < Ld; ++l) { addA((size_t)Wcap * Gcap * CTX * n * sizeof(T)); addA((size_t)Wcap * Gcap * CTX * n * sizeof(T)); }
+    addA((size_t)RD * n * 4); addA((size_t)RD * n * sizeof(T)); addA((size_t)RD * n * sizeof(T)); addA((size_t)RD * n * sizeof(T));
+    addA((size_t)RD * 4 * n * sizeof(T));
+    addA((size_t)RD * nh * NSPLIT * 64 * 4); addA((size_t)RD * nh * NSPLIT * 4); addA((size_t)RD * nh * NSPLIT * 4);
+    addA((size_t)LR * V * 4); addA((size_t)2 * Wcap * V * 4); addA(Wcap * 4);
+    for (int i = 0; i < 9; ++i) addA(RD * 4);
+    for (int i = 0; i < 5; ++i) addA(RD * 4);
+    addA(Ld * nh * 4);
+    addA(((V + 31) / 32) * 4);
+    addA(Wcap * 8); addA(Wcap * 4);
+    // state
+    addA((size_t)Wcap * Gcap * HCTX * 4); addA((size_t)Wcap * Gcap * CTX * 4);
+    for (int i = 0; i < 5; ++i) addA(Wcap * 4);
+    addA(Wcap * Gcap * 4);
+    addA(Wcap * 16 * 4); addA(Wcap * 16 * 4); addA((size_t)Wcap * 16 * HCTX * 4);
+    addA((size_t)Wcap * Gcap * KC * 4); addA((size_t)Wcap * Gcap * KC * 4);
+    addA(64);
+    HIPCHK(hipMalloc(&abase, ab));
+    HIPCHK(hipMemset(abase, 0, ab));
+    aa.base = (char*)abase;
+    aa.cap = ab;
+    auto ta = [&](size_t elems) { return (T*)aa.take(elems * sizeof(T)); };
+    auto fa = [&](size_t elems) { return (float*)aa.take(elems * 4); };
+    auto ia = [&](size_t elems) { return (int*)aa.take(elems * 4); };
+    melT = ta((size_t)WE * MROWS * nm); h1 = ta((size_t)WE * H1ROWS * n);
+    x_e = fa((size_t)WE * 1500 * n); xn_e = ta((size_t)WE * 1500 * n); qkv_e = ta((size_t)WE * 1500 * 3 * n);
+    att_e = ta((size_t)WE * 1500 * n); hm_e = ta((size_t)WE * 1500 * 4 * n);
+    xa = ta((size_t)Wcap * 1500 * n);
+    ckv = ta((size_t)2 * Ld * Wcap * 1500 * n);
+    kc.resize(Ld); vc.resize(Ld);
+    for (int l = 0; l < Ld; ++l) { kc[l] = ta((size_t)Wcap * Gcap * CTX * n); vc[l] = ta((size_t)Wcap * Gcap * CTX * n); }
+    x_d = fa((size_t)RD * n); xn_d = ta((size_t)RD * n); q_d = ta((size_t)RD * n); att_d = ta((size_t)RD * n);
+    hm_d = ta((size_t)RD * 4 * n);
+    po = fa((size_t)RD * nh * NSPLIT * 64); pm = fa((size_t)RD * nh * NSPLIT); pl = fa((size_t)RD * nh * NSPLIT);
+    logits = fa((size_t)LR * V); logits2 = fa((size_t)2 * Wcap * V); nsp = fa(Wcap);
+    row_tok = ia(RD); row_pos = ia(RD); row_win = ia(RD); row_slot = ia(RD); win_row0 = ia(RD); win_nrows = ia(RD);
+    win_slot = ia(RD); rows_in = ia(RD); src_rows = ia(RD);
+    st_row_win = ia(RD); st_row_slot = ia(RD); st_win_row0 = ia(RD); st_win_nrows = ia(RD); st_win_slot = ia(RD);
+    qk_map = ia(Ld * nh);
+    suppress = (unsigned*)ia((V + 31) / 32);
+    d_seeks = (int64_t*)aa.take(Wcap * 8); d_segs = ia(Wcap);
+    S.hist = ia((size_t)Wcap * Gcap * HCTX); S.anc = ia((size_t)Wcap * Gcap * CTX);
+    S.len = ia(Wcap); S.sample_begin = ia(Wcap); S.step = ia(Wcap); S.done = ia(Wcap); S.fin_n = ia(Wcap);
+    S.sum_lp = fa(Wcap * Gcap);
+    S.fin_score = fa(Wcap * 16); S.fin_len = ia(Wcap * 16); S.fin_tok = ia((size_t)Wcap * 16 * HCTX);
+    S.cand_val = fa((size_t)Wcap * Gcap * KC); S.cand_idx = ia((size_t)Wcap * Gcap * KC);
+    if (!S.cand_idx) return fail(-3, "activation arena overflow");
+    S.nw = Wcap; S.G = 1; S.ctx = CTX; S.hctx = HCTX; S.maxc = 16;
+    HIPCHK(hipMalloc(&d_gmax, 64));
+    d_gmax_f = (float*)(d_gmax + 4);
+    return 0;
+  }
+
+  // ------------------------------------------------------------ weights
+  int up(void* dst, const std::vector<T>& h) {
+    HIPCHK(hipMemcpy(dst, h.data(), h.size() * sizeof(T), hipMemcpyHostToDevice));
+    return 0;
+  }
+  int upf(float* dst, const float* src, size_t cnt, float scale = 1.f) {
+    if (scale == 1.f) {
+      HIPCHK(hipMemcpy(dst, src, cnt * 4, hipMemcpyHostToDevice));
+      return 0;
+    }
+    std::vector<float> t(src, src + cnt);
+    for (auto& v : t) v *= scale;
+    HIPCHK(hipMemcpy(dst, t.data(), cnt * 4, hipMemcpyHostToDevice));
+    return 0;
+  }
+  int upT(T* dst, const float* src, size_t cnt, float scale = 1.f) {
+    std::vector<T> t(cnt);
+    for (size_t i = 0; i < cnt; ++i) t[i] = (T)(src[i] * scale);
+    return up(dst, t);
+  }
+
+  int load(const std::string& name, const float* data, const int64_t* shape, int ndim) override {
+    auto numel = [&]() { int64_t c = 1; for (int i = 0; i < ndim; ++i) c *= shape[i]; return (size_t)c; };
+    auto need = [&](std::initializer_list<int64_t> want) -> int {
+      if ((int)want.size() != ndim) return fail(-4, name + ": bad rank");
+      int i = 0;
+      for (auto w : want)
+        if (shape[i++] != w) return fail(-4, name + ": bad shape");
+      return 0;
+    };
+    const size_t n = ns;
+    const float kscale = 0.125f;  // (64)^-0.5: encoder key (encoder.py:38), decoder query (decoder.py:20)
+    int rc = 0;
+    if (name == "encoder.conv1.weight") {
+      TRY(need({(int64_t)n, nm, 3}));
+      std::vector<float> t(n * K1p, 0.f);  // [o][j*nm + c] = w[o][c][j]
+      for (size_t o = 0; o < n; ++o)
+        for (int c = 0; c < nm; ++c)
+          for (int j = 0; j < 3; ++j) t[o * K1p + j * nm + c] = data[(o * nm + c) * 3 + j];
+      rc = upT(conv1_w, t.data(), t.size());
+    } else if (name == "encoder.conv1.bias") { TRY(need({(int64_t)n})); rc = upf(conv1_b, data, n); }
+    else if (name == "encoder.conv2.weight") {
+      TRY(need({(int64_t)n, (int64_t)n, 3}));
+      std::vector<float> t(n * 3 * n);
+      for (size_t o = 0; o < n; ++o)
+        for (size_t c = 0; c < n; ++c)
+          for (int j = 0; j < 3; ++j) t[o * 3 * n + j * n + c] = data[(o * n + c) * 3 + j];
+      rc = upT(conv2_w, t.data(), t.size());
+    } else if (name == "encoder.conv2.bias") { TRY(need({(int64_t)n})); rc = upf(conv2_b, data, n); }
+    else if (name == "encoder.positional_embedding") { TRY(need({1500, (int64_t)n})); rc = upf(pos_enc, data, 1500 * n); }
+    else if (name == "encoder.ln_post.weight") { TRY(need({(int64_t)n})); rc = upf(lnp_g, data, n); }
+    else if (name == "encoder.ln_post.bias") { TRY(need({(int64_t)n})); rc = upf(lnp_b, data, n); }
+    else if (name == "decoder.token_embedding.weight") { TRY(need({V, (int64_t)n})); rc = upT(E, data, (size_t)V * n); }
+    else if (name == "decoder.positional_embedding") { TRY(need({CTX, (int64_t)n})); rc = upT(Pdec, data, CTX * n); }
+    else if (name == "decoder.ln.weight") { TRY(need({(int64_t)n})); rc = upf(ln_g, data, n); }
+    else if (name == "decoder.ln.bias") { TRY(need({(int64_t)n})); rc = upf(ln_b, data, n); }
+    else {
+      int l = -1;
+      char part[128];
+      const bool is_enc = sscanf(name.c_str(), "encoder.blocks.%d.%127s", &l, part) == 2;
+      const bool is_dec = !is_enc && sscanf(name.c_str(), "decoder.blocks.%d.%127s", &l, part) == 2;
+      if (!is_enc && !is_dec) return fail(-5, "unknown tensor " + name);
+      const std::string p(part);
+      if (is_enc) {
+        if (l < 0 || l >= La) return fail(-5, "layer out of range " + name);
+        auto& e = enc[l];
+        if (p == "attn.query.weight") { TRY(need({(int64_t)n, (int64_t)n})); rc = upT(e.wqkv, data, n * n); }
+        else if (p == "attn.query.bias") { TRY(need({(int64_t)n})); rc = upf(e.bqkv, data, n); }
+        else if (p == "attn.key.weight") { TRY(need({(int64_t)n, (int64_t)n})); rc = upT(e.wqkv + n * n, data, n * n, kscale); }
+        else if (p == "attn.value.weight") { TRY(need({(int64_t)n, (int64_t)n})); rc = upT(e.wqkv + 2 * n * n, data, n * n); }
+        else if (p == "attn.value.bias") { TRY(need({(int64_t)n})); rc = upf(e.bqkv + 2 * n, data, n); }
+        else if (p == "attn.out.weight") { TRY(need({(int64_t)n, (int64_t)n})); rc = upT(e.wo, data, n * n); }
+        else if (p == "attn.out.bias") { TRY(need({(int64_t)n})); rc = upf(e.bo, data, n); }
+        else if (p == "attn_ln.weight") { TRY(need({(int64_t)n})); rc = upf(e.ln1_g, data, n); }
+        else if (p == "attn_ln.bias") { TRY(need({(int64_t)n})); rc = upf(e.ln1_b, data, n); }
+        else if (p == "mlp_ln.weight") { TRY(need({(int64_t)n})); rc = upf(e.ln2_g, data, n); }
+        else if (p == "mlp_ln.bias") { TRY(need({(int64_t)n})); rc = upf(e.ln2_b, data, n); }
+        else if (p == "mlp.0.weight") { TRY(need({4 * (int64_t)n, (int64_t)n})); rc = upT(e.w1, data, 4 * n * n); }
+        else if (p == "mlp.0.bias") { TRY(need({4 * (int64_t)n})); rc = upf(e.b1, data, 4 * n); }
+        else if (p == "mlp.2.weight") { TRY(need({(int64_t)n, 4 * (int64_t)n})); rc = upT(e.w2, data, 4 * n * n); }
+        else if (p == "mlp.2.bias") { TRY(need({(int64_t)n})); rc = upf(e.b2, data, n); }
+        else return fail(-5, "unknown tensor " + name);
+      } else {
+        if (l < 0 || l >= Ld) return fail(-5, "layer out of range " + name);
+        auto& e = dec[l];
+        T* ck = ckv_w + (size_t)(2 * l) * n * n;
+        if (p == "attn.query.weight") { TRY(need({(int64_t)n, (int64_t)n})); rc = upT(e.wqkv, data, n * n, kscale); }
+        else if (p == "attn.query.bias") { TRY(need({(int64_t)n})); rc = upf(e.bqkv, data, n, kscale); }
+        else if (p == "attn.key.weight") { TRY(need({(int64_t)n, (int64_t)n})); rc = upT(e.wqkv + n * n, data, n * n); }
+        else if (p == "attn.value.weight") { TRY(need({(int64_t)n, (int64_t)n})); rc = upT(e.wqkv + 2 * n * n, data, n * n); }
+        else if (p == "attn.value.bias") { TRY(need({(int64_t)n})); rc = upf(e.bqkv + 2 * n, data, n); }
+        else if (p == "attn.out.weight") { TRY(need({(int64_t)n, (int64_t)n})); rc = upT(e.wo, data, n * n); }
+        else if (p == "attn.out.bias") { TRY(need({(int64_t)n})); rc = upf(e.bo, data, n); }
+        else if (p == "attn_ln.weight") { TRY(need({(int64_t)n})); rc = upf(e.ln1_g, data, n); }
+        else if (p == "attn_ln.bias") { TRY(need({(int64_t)n})); rc = upf(e.ln1_b, data, n); }
+        else if (p == "cross_attn.query.weight") { TRY(need({(int64_t)n, (int64_t)n})); rc = upT(e.wqx, data, n * n, kscale); }
+        else if (p == "cross_attn.query.bias") { TRY(need({(int64_t)n})); rc = upf(e.bqx, data, n, kscale); }
+        else if (p == "cross_attn.key.weight") { TRY(need({(int64_t)n, (int64_t)n})); rc = upT(ck, data, n * n); }
+        else if (p == "cross_attn.value.weight") { TRY(need({(int64_t)n, (int64_t)n})); rc = upT(ck + n * n, data, n * n); }
+        else if (p == "cross_attn.value.bias") { TRY(need({(int64_t)n})); rc = upf(ckv_b + (2 * l + 1) * n, data, n); }
+        else if (p == "cross_attn.out.weight") { TRY(need({(int64_t)n, (int64_t)n})); rc = upT(e.wox, data, n * n); }
+        else if (p == "cross_attn.out.bias") { TRY(need({(int64_t)n})); rc = upf(e.box, data, n); }
+        else if (p == "cross_attn_ln.weight") { TRY(need({(int64_t)n})); rc = upf(e.lnx_g, data, n); }
+        else if (p == "cross_attn_ln.bias") { TRY(need({(int64_t)n})); rc = upf(e.lnx_b, data, n); }
+        else if (p == "mlp_ln.weight") { TRY(need({(int64_t)n})); rc = upf(e.ln2_g, data, n); }
+        else if (p == "mlp_ln.bias") { TRY(need({(int64_t)n})); rc = upf(e.ln2_b, data, n); }
+        else if (p == "mlp.0.weight") { TRY(need({4 * (int64_t)n, (int64_t)n})); rc = upT(e.w1, data, 4 * n * n); }
+        else if (p == "mlp.0.bias") { TRY(need({4 * (int64_t)n})); rc = upf(e.b1, data, 4 * n); }
+        else if (p == "mlp.2.weight") { TRY(need({(int64_t)n, 4 * (int64_t)n})); rc = upT(e.w2, data, 4 * n * n); }
+        else if (p == "mlp.2.bias") { TRY(need({(int64_t)n})); rc = upf(e.b2, data, n); }
+        else return fail(-5, "unknown tensor " + name);
+      }
+    }
+    if (rc) return rc;
+    (void)numel;
+    loaded.insert(name);
+    return 0;
+  }
+
+  int finalize() override {
+    if (loaded.size() != expected)
+      return fail(-6, "loaded " + std::to_string(loaded.size()) + " of " + std::to_string(expected) + " tensors");
+    HIPCHK(hipDeviceSynchronize());
+    finalized = true;
+    return 0;
+  }
+
+  // ------------------------------------------------------------ GEMM helper
+  int gemm(const void* X, int ldx, const T* W, const float* bias, int M, int N, int K, int epi, GemmArgs a) {
+    a.X = X; a.ldx = ldx; a.W = W; a.bias = bias; a.M = M; a.N = N; a.K = K;
+    if (a.x_group_rows == (1 << 30)) a.x_group_rows = std::max(M, 1);
+    const int rc = launch_gemm<T>(a, epi, st);
+    if (rc) return fail(-20, "gemm launch failed code " + std::to_string(rc) + " M=" + std::to_string(M) +
+                                 " N=" + std::to_string(N) + " K=" + std::to_string(K));
+    return 0;
+  }
+
+  // ------------------------------------------------------------ mel
+  int log_mel(const float* audio, int64_t n, int64_t pad, int n_mels, int normalize, int64_t* nf) override {
+    if (!h_filters.count(n_mels)) return fail(-7, "mel filters for n_mels=" + std::to_string(n_mels) + " not set");
+    if (n + pad <= 200) return fail(-7, "audio too short for reflect padding");
+    const int64_t frames = (n + pad) / 160;
+    if ((size_t)n > audio_cap) {
+      if (d_audio) hipFree(d_audio);
+      audio_cap = std::max<size_t>(n, 16000);
+      HIPCHK(hipMalloc(&d_audio, audio_cap * 4));
+    }
+    const size_t need = (size_t)n_mels * frames;
+    if (need > mel_cap) {
+      if (d_mel) hipFree(d_mel);
+      mel_cap = need;
+      HIPCHK(hipMalloc(&d_mel, mel_cap * 4));
+    }
+    hipEventRecord(tm.a, st);
+    HIPCHK(hipMemcpyAsync(d_audio, audio, n * 4, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemsetAsync(d_gmax, 0, 16, st));
+    launch_mel(d_audio, n, n + pad, 0, frames, d_filters[n_mels], n_mels, d_mel, frames, d_gmax, st);
+    if (normalize) launch_mel_norm(d_mel, frames, frames, n_mels, d_gmax, nullptr, st);
+    hipEventRecord(tm.b, st);
+    HIPCHK(hipStreamSynchronize(st));
+    float ms = 0;
+    hipEventElapsedTime(&ms, tm.a, tm.b);
+    stats[0] += ms;
+    mel_frames = frames;
+    mel_nm = n_mels;
+    *nf = frames;
+    return 0;
+  }
+  std::map<int, std::vector<float>> h_filters;
+  int mel_max(float* g) override {
+    unsigned u = 0;
+    HIPCHK(hipMemcpy(&u, d_gmax, 4, hipMemcpyDeviceToHost));
+    const unsigned v = (u & 0x80000000u) ? (u & 0x7fffffffu) : ~u;
+    memcpy(g, &v, 4);
+    return 0;
+  }
+  int mel_normalize(float g) override {
+    HIPCHK(hipMemcpyAsync(d_gmax_f, &g, 4, hipMemcpyHostToDevice, st));
+    launch_mel_norm(d_mel, mel_frames, mel_frames, mel_nm, d_gmax, d_gmax_f, st);
+    HIPCHK(hipStreamSynchronize(st));
+    return 0;
+  }
+  int mel_read(float* out, int64_t f0, int64_t nf) override {
+    if (f0 < 0 || f0 + nf > mel_frames) return fail(-8, "mel_read out of range");
+    HIPCHK(hipMemcpy2D(out, nf * 4, d_mel + f0, mel_frames * 4, nf * 4, mel_nm, hipMemcpyDeviceToHost));
+    return 0;
+  }
+  int mel_write(const float* mel, int64_t nf) override {
+    const size_t need = (size_t)nm * nf;
+    if (need > mel_cap) {
+      if (d_mel) hipFree(d_mel);
+      mel_cap = need;
+      HIPCHK(hipMalloc(&d_mel, mel_cap * 4));
+    }
+    HIPCHK(hipMemcpy(d_mel, mel, need * 4, hipMemcpyHostToDevice));
+    mel_frames = nf;
+    mel_nm = nm;
+    return 0;
+  }
+
+  // ------------------------------------------------------------ encoder
+  int encode_chunk(int s0, int we) {
+    const int n = ns;
+    GemmArgs g;
+    // mel windows -> time-major (T), conv1 as overlapping-row GEMM (lda = n_mels)
+    launch_mel_windows<T>(d_mel, mel_frames, nm, d_seeks + s0, d_segs + s0, melT, (int64_t)MROWS * nm, MROWS, we, st);
+    g = GemmArgs();
+    g.x_group_rows = 3000; g.x_group_stride = (int64_t)MROWS * nm;
+    g.out = h1; g.ldo = n; g.out_group_stride = (int64_t)H1ROWS * n; g.out_row_off = 1;
+    TRY(gemm(melT, nm, conv1_w, conv1_b, we * 3000, n, K1p, EPI_STORE_GELU, g));
+    launch_zero_rows<T>(h1, (int64_t)H1ROWS * n, n, 0, H1ROWS - 1, we, st);
+    // conv2 (stride 2): row t reads padded rows 2t..2t+2 -> lda = 2n; + GELU + positional embedding
+    g = GemmArgs();
+    g.x_group_rows = 1500; g.x_group_stride = (int64_t)H1ROWS * n;
+    g.out_f32 = x_e; g.ldo = n; g.pos = pos_enc;
+    TRY(gemm(h1, 2 * n, conv2_w, conv2_b, we * 1500, n, 3 * n, EPI_GELU_POS, g));
+    const int M = we * 1500;
+    for (int l = 0; l < La; ++l) {
+      auto& e = enc[l];
+      launch_layernorm<T>(x_e, xn_e, e.ln1_g, e.ln1_b, M, n, 1e-7f, nullptr, st);
+      g = GemmArgs(); g.out = qkv_e; g.ldo = 3 * n;
+      TRY(gemm(xn_e, n, e.wqkv, e.bqkv, M, 3 * n, n, EPI_STORE, g));
+      launch_attn_enc<T>(qkv_e, 3 * n, n, nh, 1500, we, (int64_t)1500 * 3 * n, att_e, (int64_t)1500 * n, st);
+      g = GemmArgs(); g.out_f32 = x_e; g.ldo = n;
+      TRY(gemm(att_e, n, e.wo, e.bo, M, n, n, EPI_RESID, g));
+      launch_layernorm<T>(x_e, xn_e, e.ln2_g, e.ln2_b, M, n, 1e-7f, nullptr, st);
+      g = GemmArgs(); g.out = hm_e; g.ldo = 4 * n;
+      TRY(gemm(xn_e, n, e.w1, e.b1, M, 4 * n, n, EPI_STORE_GELU, g));
+      g = GemmArgs(); g.out_f32 = x_e; g.ldo = n;
+      TRY(gemm(hm_e, 4 * n, e.w2, e.b2, M, n, 4 * n, EPI_RESID, g));
+    }
+    T* xa_s = xa + (size_t)s0 * 1500 * n;
+    launch_layernorm<T>(x_e, xa_s, lnp_g, lnp_b, M, n, 1e-7f, nullptr, st);
+    // cross-KV for every decoder layer in one GEMM, written head-split [l2][slot][h][t][64]
+    g = GemmArgs();
+    g.x_group_rows = 1500; g.x_group_stride = (int64_t)1500 * n;
+    g.out = ckv; g.hs_state = n; g.hs_heads = nh; g.hs_T = 1500; g.hs_nslots = Wcap; g.hs_slot0 = s0;
+    TRY(gemm(xa_s, n, ckv_w, ckv_b, M, 2 * Ld * n, n, EPI_HEADSPLIT, g));
+    return 0;
+  }
+
+  int encode(int n_win, const int64_t* seeks, const int* segs) override {
+    if (!finalized) return fail(-9, "weights not finalized");
+    if (n_win < 1 || n_win > Wcap) return fail(-9, "n_win out of range");
+    if (!d_mel || mel_nm != nm) return fail(-9, "no mel of the model's n_mels in the context");
+    for (int i = 0; i < n_win; ++i)
+      if (seeks[i] < 0 || seeks[i] >= mel_frames || segs[i] < 1) return fail(-9, "bad window");
+    hipEventRecord(tm.a, st);
+    HIPCHK(hipMemcpyAsync(d_seeks, seeks, n_win * 8, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(d_segs, segs, n_win * 4, hipMemcpyHostToDevice, st));
+    const int WE = std::min(Wcap, ENC_CHUNK);
+    for (int s0 = 0; s0 < n_win; s0 += WE) TRY(encode_chunk(s0, std::min(WE, n_win - s0)));
+    hipEventRecord(tm.b, st);
+    HIPCHK(hipStreamSynchronize(st));
+    float ms = 0;
+    hipEventElapsedTime(&ms, tm.a, tm.b);
+    stats[1] += ms;
+    stats[5] += n_win;
+    HIPCHK(hipGetLastError());
+    return 0;
+  }
+
+  int read_xa(int slot, float* out) override {
+    if (slot < 0 || slot >= Wcap) return fail(-10, "slot");
+    const size_t cnt = (size_t)1500 * ns;
+    std::vector<T> h(cnt);
+    HIPCHK(hipMemcpy(h.data(), xa + (size_t)slot * cnt, cnt * sizeof(T), hipMemcpyDeviceToHost));
+    for (size_t i = 0; i < cnt; ++i) out[i] = (float)h[i];
+    return 0;
+  }
+  int read_ckv(int slot, int layer, float* k, float* v) override {
+    if (slot < 0 || slot >= Wcap || layer < 0 || layer >= Ld) return fail(-10, "slot/layer");
+    const size_t per = (size_t)nh * 1500 * 64;
+    std::vector<T> h(per);
+    for (int kv = 0; kv < 2; ++kv) {
+      const T* src = ckv + ((size_t)(2 * layer + kv) * Wcap + slot) * per;
+      HIPCHK(hipMemcpy(h.data(), src, per * sizeof(T), hipMemcpyDeviceToHost));
+      float* o = kv ? v : k;
+      for (size_t i = 0; i < per; ++i) o[i] = (float)h[i];
+    }
+    return 0;
+  }
+
+  // ------------------------------------------------------------ decoder layers
+  // R rows of x_d (f32 residual); rw/rs/rp: row window / beam slot / position
+  // ancG: beams per window in the anc table layout [w][ancG][ctx]; KV slots use Gcap
+  int dec_layers(int R, const int* rw, const int* rs, const int* rp, int ancG, int nwin, const int* wr0, const int* wnr,
+                 const int* wsl, float* aqk, const int* qkmap, int qkrows) {
+    const int n = ns;
+    GemmArgs g;
+    for (int l = 0; l < Ld; ++l) {
+      auto& e = dec[l];
+      launch_layernorm<T>(x_d, xn_d, e.ln1_g, e.ln1_b, R, n, 1e-5f, nullptr, st);
+      g = GemmArgs();
+      g.out = q_d; g.ldo = n; g.hs_state = n; g.hs_heads = nh;
+      g.row_win = rw; g.row_slot = rs; g.row_pos = rp; g.kc = kc[l]; g.vc = vc[l]; g.kv_beams = Gcap; g.kv_ctx = CTX;
+      TRY(gemm(xn_d, n, e.wqkv, e.bqkv, R, 3 * n, n, EPI_QKV_DEC, g));
+      launch_self_attn<T>(q_d, n, kc[l], vc[l], rw, rs, rp, S.anc, ancG, Gcap, nh, CTX, att_d, n, R, st);
+      g = GemmArgs(); g.out_f32 = x_d; g.ldo = n;
+      TRY(gemm(att_d, n, e.wo, e.bo, R, n, n, EPI_RESID, g));
+      launch_layernorm<T>(x_d, xn_d, e.lnx_g, e.lnx_b, R, n, 1e-5f, nullptr, st);
+      g = GemmArgs(); g.out = q_d; g.ldo = n;
+      TRY(gemm(xn_d, n, e.wqx, e.bqx, R, n, n, EPI_STORE, g));
+      const T* ck = ckv + (size_t)(2 * l) * Wcap * 1500 * n;
+      const T* cv = ckv + (size_t)(2 * l + 1) * Wcap * 1500 * n;
+      launch_cross_attn<T>(q_d, n, ck, cv, 1500, nh, NSPLIT, nwin, wr0, wnr, wsl, (int64_t)1500 * n, po, pm, pl, att_d,
+                           n, R, aqk, qkmap ? qkmap + l * nh : nullptr, qkrows, st);
+      g = GemmArgs(); g.out_f32 = x_d; g.ldo = n;
+      TRY(gemm(att_d, n, e.wox, e.box, R, n, n, EPI_RESID, g));
+      launch_layernorm<T>(x_d, xn_d, e.ln2_g, e.ln2_b, R, n, 1e-5f, nullptr, st);
+      g = GemmArgs(); g.out = hm_d; g.ldo = 4 * n;
+      TRY(gemm(xn_d, n, e.w1, e.b1, R, 4 * n, n, EPI_STORE_GELU, g));
+      g = GemmArgs(); g.out_f32 = x_d; g.ldo = n;
+      TRY(gemm(hm_d, 4 * n, e.w2, e.b2, R, n, 4 * n, EPI_RESID, g));
+    }
+    return 0;
+  }
+
+  int vocab(const float* xrows_src, const int* rows_sel, int R, float* out) {
+    // final LayerNorm (eps 1e-5) on selected rows, then logits = x E^T (decoder.py:238-240, 316-320)
+    launch_layernorm<T>(xrows_src, xn_d, ln_g, ln_b, R, ns, 1e-5f, rows_sel, st);
+    GemmArgs g;
+    g.out_f32 = out; g.ldo = V;
+    return gemm(xn_d, ns, E, nullptr, R, V, ns, EPI_F32_COLS, g);
+  }
+
+  // ------------------------------------------------------------ decoding
+  int set_opts(const wh_decode_opts* o) {
+    if (o->group < 1 || o->group > Gcap) return fail(-11, "group exceeds context max_group");
+    O = DecOpts();
+    O.V = V; O.eot = o->eot; O.ts_begin = o->timestamp_begin; O.no_ts = o->no_timestamps;
+    O.n_blank = std::min(o->n_blank, 3);
+    for (int i = 0; i < O.n_blank; ++i) O.blank[i] = o->blank[i];
+    O.blank[O.n_blank] = o->eot;  // SuppressBlank masks encode(" ") + [eot]
+    O.n_blank += 1;
+    O.suppress_blank = o->suppress_blank; O.timestamps = o->timestamps; O.max_initial = o->max_initial;
+    O.beam = o->beam; O.sample_len = o->sample_len; O.n_ctx = CTX; O.temperature = o->temperature; O.seed = o->seed;
+    std::vector<unsigned> mask((V + 31) / 32, 0u);
+    for (int i = 0; i < o->n_suppress; ++i) {
+      const int t = o->suppress[i];
+      if (t >= 0 && t < V) mask[t >> 5] |= 1u << (t & 31);
+    }
+    HIPCHK(hipMemcpyAsync(suppress, mask.data(), mask.size() * 4, hipMemcpyHostToDevice, st));
+    O.suppress = o->n_suppress > 0 ? suppress : nullptr;
+    maxc = o->beam ? (int)std::lround(o->group * (o->patience > 0 ? o->patience : 1.0f)) : 0;
+    if (o->beam && (maxc < 1 || maxc > 16)) return fail(-11, "max_candidates out of range (1..16)");
+    S.G = o->group;
+    S.maxc = 16;
+    return 0;
+  }
+
+  int prefill(int w0, int nw, const std::vector<int>& toks, const std::vector<int>& nin, const int* sot_index,
+              bool first_update_rows) {
+    // rows of windows w0..w0+nw-1, all in beam slot 0; cross attention per window
+    std::vector<int> rt, rp, rw, rs, wr0(nw), wnr(nw), wsl(nw), sel;
+    for (int i = 0; i < nw; ++i) {
+      wr0[i] = (int)rt.size();
+      wnr[i] = nin[i];
+      wsl[i] = w0 + i;
+      for (int p = 0; p < nin[i]; ++p) {
+        rt.push_back(toks[(size_t)i * HCTX + p]);
+        rp.push_back(p);
+        rw.push_back(w0 + i);
+        rs.push_back(0);
+      }
+      sel.push_back(wr0[i] + sot_index[w0 + i]);
+      sel.push_back(wr0[i] + nin[i] - 1);
+    }
+    const int R = (int)rt.size();
+    HIPCHK(hipMemcpyAsync(row_tok, rt.data(), R * 4, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(row_pos, rp.data(), R * 4, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(row_win, rw.data(), R * 4, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(row_slot, rs.data(), R * 4, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(win_row0, wr0.data(), nw * 4, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(win_nrows, wnr.data(), nw * 4, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(win_slot, wsl.data(), nw * 4, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(rows_in, sel.data(), sel.size() * 4, hipMemcpyHostToDevice, st));
+    launch_embed<T>(E, Pdec, ns, row_tok, row_pos, nullptr, nullptr, 1, HCTX, CTX - 1, x_d, R, st);
+    TRY(dec_layers(R, row_win, row_slot, row_pos, S.G, nw, win_row0, win_nrows, win_slot, nullptr, nullptr, 0));
+    TRY(vocab(x_d, rows_in, 2 * nw, logits2 + (size_t)2 * w0 * V));
+    (void)first_update_rows;
+    // the host vectors must outlive the async copies
+    HIPCHK(hipStreamSynchronize(st));
+    return 0;
+  }
+
+  int decode_begin(int n_win, const wh_decode_opts* o, const int* init, const int* n_init, int max_init,
+                   const int* sot_index) override {
+    if (!finalized) return fail(-9, "weights not finalized");
+    if (n_win < 1 || n_win > Wcap) return fail(-11, "n_win out of range");
+    TRY(set_opts(o));
+    const int G = o->group;
+    hipEventRecord(tm.a, st);
+    // host-side initial state
+    std::vector<int> hist((size_t)n_win * Gcap * HCTX, 0), anc((size_t)n_win * Gcap * CTX, 0), toks((size_t)n_win * HCTX, 0);
+    std::vector<int> nin(n_win), lens(n_win), zeros(n_win, 0);
+    for (int w = 0; w < n_win; ++w) {
+      nin[w] = n_init[w];
+      if (nin[w] < 1 || nin[w] > CTX - 1) return fail(-11, "initial token count out of range");
+      if (sot_index[w] < 0 || sot_index[w] >= nin[w]) return fail(-11, "bad sot_index");
+      for (int p = 0; p < nin[w]; ++p) {
+        const int t = init[(size_t)w * max_init + p];
+        if (t < 0 || t >= V) return fail(-11, "initial token out of vocabulary");
+        toks[(size_t)w * HCTX + p] = t;
+      }
+    }
+    S.G = G;
+    // history / ancestry laid out with the runtime group G ([w][G][..])
+    for (int w = 0; w < n_win; ++w)
+      for (int b = 0; b < G; ++b) {
+        for (int p = 0; p < nin[w]; ++p) hist[((size_t)w * G + b) * HCTX + p] = toks[(size_t)w * HCTX + p];
+        for (int p = 0; p < CTX; ++p) anc[((size_t)w * G + b) * CTX + p] = p < nin[w] ? 0 : b;
+      }
+    // prefill (anc must be in place first: prefill rows read slot 0 through it)
+    HIPCHK(hipMemcpyAsync(S.anc, anc.data(), (size_t)n_win * G * CTX * 4, hipMemcpyHostToDevice, st));
+    // prefill runs with kv_beams = Gcap layout; rows use slot 0
+    for (int w0 = 0; w0 < n_win;) {
+      int rows = 0, nw = 0;
+      while (w0 + nw < n_win && (nw == 0 || rows + nin[w0 + nw] <= PRE_ROWS)) rows += nin[w0 + nw++];
+      if (rows > PRE_ROWS) return fail(-11, "prefill rows exceed buffer");
+      std::vector<int> sub_toks(toks.begin() + (size_t)w0 * HCTX, toks.begin() + (size_t)(w0 + nw) * HCTX);
+      std::vector<int> sub_n(nin.begin() + w0, nin.begin() + w0 + nw);
+      TRY(prefill(w0, nw, sub_toks, sub_n, sot_index, true));
+      w0 += nw;
+    }
+    // no_speech prob from the sot row of each window (decoding.py:716-720)
+    if (o->no_speech >= 0) launch_no_speech(logits2, 2 * V, n_win, V, o->no_speech, nsp, st);
+    // last-row logits replicated to the G rows of each window
+    std::vector<int> src(n_win);
+    for (int w = 0; w < n_win; ++w) src[w] = 2 * w + 1;
+    HIPCHK(hipMemcpyAsync(src_rows, src.data(), n_win * 4, hipMemcpyHostToDevice, st));
+    launch_broadcast_rows(logits2, V, src_rows, logits, V, G, n_win, V, st);
+    // decode state
+    HIPCHK(hipMemcpyAsync(S.hist, hist.data(), (size_t)n_win * G * HCTX * 4, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(S.len, nin.data(), n_win * 4, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(S.sample_begin, nin.data(), n_win * 4, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemsetAsync(S.step, 0, n_win * 4, st));
+    HIPCHK(hipMemsetAsync(S.done, 0, n_win * 4, st));
+    HIPCHK(hipMemsetAsync(S.fin_n, 0, n_win * 4, st));
+    HIPCHK(hipMemsetAsync(S.sum_lp, 0, n_win * G * 4, st));
+    S.maxc = std::max(maxc, 1);
+    maxc_stride = S.maxc;
+    // static step-row metadata: row r = w*G + b
+    std::vector<int> srw(n_win * G), srs(n_win * G), swr0(n_win), swnr(n_win, G), swsl(n_win);
+    for (int w = 0; w < n_win; ++w) {
+      swr0[w] = w * G;
+      swsl[w] = w;
+      for (int b = 0; b < G; ++b) { srw[w * G + b] = w; srs[w * G + b] = b; }
+    }
+    HIPCHK(hipMemcpyAsync(st_row_win, srw.data(), srw.size() * 4, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(st_row_slot, srs.data(), srs.size() * 4, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(st_win_row0, swr0.data(), n_win * 4, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(st_win_nrows, swnr.data(), n_win * 4, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(st_win_slot, swsl.data(), n_win * 4, hipMemcpyHostToDevice, st));
+    // the self-KV cache uses [w][Gcap][..] slots; the anc table uses [w][G][..]
+    cur_nwin = n_win;
+    cur_G = G;
+    // first update on the prefill logits (decoding.py:713-733, i == 0)
+    launch_logit_rows(logits, V, S, O, n_win, st);
+    launch_merge(S, O, n_win, st);
+    hipEventRecord(tm.b, st);
+    HIPCHK(hipStreamSynchronize(st));
+    HIPCHK(hipGetLastError());
+    float ms = 0;
+    hipEventElapsedTime(&ms, tm.a, tm.b);
+    stats[2] += ms;
+    return 0;
+  }
+
+  // one decoder step for the current batch (graph body)
+  int step_body() {
+    const int R = cur_nwin * cur_G;
+    launch_embed<T>(E, Pdec, ns, nullptr, row_pos, S.hist, S.len, cur_G, HCTX, CTX - 1, x_d, R, st);
+    TRY(dec_layers(R, st_row_win, st_row_slot, row_pos, cur_G, cur_nwin, st_win_row0, st_win_nrows, st_win_slot,
+                   nullptr, nullptr, 0));
+    TRY(vocab(x_d, nullptr, R, logits));
+    launch_logit_rows(logits, V, S, O, cur_nwin, st);
+    launch_merge(S, O, cur_nwin, st);
+    return 0;
+  }
+
+  int ensure_graph() {
+    std::vector<char> key(sizeof(DecOpts) + sizeof(DecState) + 8);
+    memcpy(key.data(), &O, sizeof(DecOpts));
+    memcpy(key.data() + sizeof(DecOpts), &S, sizeof(DecState));
+    memcpy(key.data() + sizeof(DecOpts) + sizeof(DecState), &cur_nwin, 4);
+    memcpy(key.data() + sizeof(DecOpts) + sizeof(DecState) + 4, &cur_G, 4);
+    if (gexec && key == graph_key) return 0;
+    if (gexec) { hipGraphExecDestroy(gexec); gexec = nullptr; }
+    if (graph) { hipGraphDestroy(graph); graph = nullptr; }
+    HIPCHK(hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal));
+    const int rc = step_body();
+    hipGraph_t g = nullptr;
+    const hipError_t e = hipStreamEndCapture(st, &g);
+    if (rc) { if (g) hipGraphDestroy(g); return rc; }
+    if (e != hipSuccess) return fail(-12, std::string("graph capture: ") + hipGetErrorString(e));
+    graph = g;
+    HIPCHK(hipGraphInstantiate(&gexec, graph, nullptr, nullptr, 0));
+    graph_key = key;
+    return 0;
+  }
+
+  int decode_steps(int max_steps, int* n_done) override {
+    if (cur_nwin < 1) return fail(-13, "no decode in progress");
+    TRY(ensure_graph());
+    hipEventRecord(tm.a, st);
+    int steps = 0, done = 0;
+    const int chunk = 8;
+    while (steps < max_steps) {
+      const int k = std::min(chunk, max_steps - steps);
+      for (int i = 0; i < k; ++i) HIPCHK(hipGraphLaunch(gexec, st));
+      steps += k;
+      HIPCHK(hipMemcpyAsync(h_done, S.done, cur_nwin * 4, hipMemcpyDeviceToHost, st));
+      HIPCHK(hipStreamSynchronize(st));
+      done = 0;
+      for (int w = 0; w < cur_nwin; ++w) done += h_done[w] != 0;
+      if (done == cur_nwin) break;
+    }
+    hipEventRecord(tm.b, st);
+    HIPCHK(hipStreamSynchronize(st));
+    float ms = 0;
+    hipEventElapsedTime(&ms, tm.a, tm.b);
+    stats[3] += ms;
+    stats[4] += steps;
+    *n_done = done;
+    return 0;
+  }
+
+  int decode_read(int slot, int* tokens, float* slp, int* len, int* fin_n, int* fin_tok, int* fin_len,
+                  float* fin_score, float* nspo) override {
+    if (slot < 0 || slot >= cur_nwin) return fail(-14, "slot");
+    const int G = cur_G;
+    HIPCHK(hipStreamSynchronize(st));
+    if (tokens) HIPCHK(hipMemcpy(tokens, S.hist + (size_t)slot * G * HCTX, (size_t)G * HCTX * 4, hipMemcpyDeviceToHost));
+    if (slp) HIPCHK(hipMemcpy(slp, S.sum_lp + slot * G, G * 4, hipMemcpyDeviceToHost));
+    if (len) HIPCHK(hipMemcpy(len, S.len + slot, 4, hipMemcpyDeviceToHost));
+    if (fin_n) HIPCHK(hipMemcpy(fin_n, S.fin_n + slot, 4, hipMemcpyDeviceToHost));
+    const int mc = S.maxc;
+    if (fin_tok) HIPCHK(hipMemcpy(fin_tok, S.fin_tok + (size_t)slot * mc * HCTX, (size_t)mc * HCTX * 4, hipMemcpyDeviceToHost));
+    if (fin_len) HIPCHK(hipMemcpy(fin_len, S.fin_len + slot * mc, mc * 4, hipMemcpyDeviceToHost));
+    if (fin_score) HIPCHK(hipMemcpy(fin_score, S.fin_score + slot * mc, mc * 4, hipMemcpyDeviceToHost));
+    if (nspo) HIPCHK(hipMemcpy(nspo, nsp + slot, 4, hipMemcpyDeviceToHost));
+    return 0;
+  }
+
+  // Whisper.forward (model.py:110-119): all-row logits of a first pass for one window,
+  // optional raw cross-QK of alignment heads.  Uses beam slot 0 of `slot` and the anc
+  // table with a 1-beam layout; call it when no decode of that slot is in flight.
+  int prefill_logits(int slot, const int* tokens, int n, float* lg, const int* ah, int na, float* aqk) override {
+    if (!finalized) return fail(-9, "weights not finalized");
+    if (slot < 0 || slot >= Wcap || n < 1 || n > CTX) return fail(-15, "bad slot or token count");
+    for (int i = 0; i < n; ++i)
+      if (tokens[i] < 0 || tokens[i] >= V) return fail(-15, "token out of vocabulary");
+    std::vector<int> rt(tokens, tokens + n), rp(n), rw(n, slot), rs(n, 0), one0{0}, onen{n}, onesl{slot};
+    for (int i = 0; i < n; ++i) rp[i] = i;
+    std::vector<int> anc0((size_t)CTX, 0);
+    std::vector<int> map((size_t)Ld * nh, -1);
+    for (int i = 0; i < na; ++i)
+      if (ah[i] >= 0 && ah[i] < Ld * nh) map[ah[i]] = i;
+    HIPCHK(hipMemcpyAsync(row_tok, rt.data(), n * 4, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(row_pos, rp.data(), n * 4, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(row_win, rw.data(), n * 4, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(row_slot, rs.data(), n * 4, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(win_row0, one0.data(), 4, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(win_nrows, onen.data(), 4, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(win_slot, onesl.data(), 4, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(S.anc + (size_t)slot * CTX, anc0.data(), CTX * 4, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(qk_map, map.data(), map.size() * 4, hipMemcpyHostToDevice, st));
+    float* d_aqk = nullptr;
+    float* out = nullptr;
+    if (na > 0 && aqk) HIPCHK(hipMalloc((void**)&d_aqk, (size_t)na * n * 1500 * 4));
+    HIPCHK(hipMalloc((void**)&out, (size_t)n * V * 4));
+    launch_embed<T>(E, Pdec, ns, row_tok, row_pos, nullptr, nullptr, 1, HCTX, CTX - 1, x_d, n, st);
+    int rc = dec_layers(n, row_win, row_slot, row_pos, 1, 1, win_row0, win_nrows, win_slot, d_aqk,
+                        d_aqk ? qk_map : nullptr, n);
+    std::vector<int> s2(n);
+    for (int i = 0; i < n; ++i) s2[i] = i;
+    for (int r0 = 0; r0 < n && rc == 0; r0 += 128) {
+      const int rr = std::min(128, n - r0);
+      if (hipMemcpyAsync(rows_in, s2.data() + r0, rr * 4, hipMemcpyHostToDevice, st) != hipSuccess) rc = -100;
+      if (!rc) rc = vocab(x_d, rows_in, rr, out + (size_t)r0 * V);
+      if (!rc && hipStreamSynchronize(st) != hipSuccess) rc = -100;
+    }
+    if (!rc && hipMemcpyAsync(lg, out, (size_t)n * V * 4, hipMemcpyDeviceToHost, st) != hipSuccess) rc = -100;
+    if (!rc && d_aqk && hipMemcpyAsync(aqk, d_aqk, (size_t)na * n * 1500 * 4, hipMemcpyDeviceToHost, st) != hipSuccess)
+      rc = -100;
+    hipStreamSynchronize(st);
+    hipFree(out);
+    if (d_aqk) hipFree(d_aqk);
+    if (rc == -100) return fail(-100, "prefill_logits: HIP copy failed");
+    if (rc) return rc;
+    HIPCHK(hipGetLastError());
+    return 0;
+  }
+
+  int time_stage(int what, int iters, double* ms) override {
+    if (what == 0) {
+      if (cur_nwin < 1) return fail(-16, "no decode batch");
+      TRY(ensure_graph());
+      hipEventRecord(tm.a, st);
+      for (int i = 0; i < iters; ++i) HIPCHK(hipGraphLaunch(gexec, st));
+      hipEventRecord(tm.b, st);
+    } else {
+      hipEventRecord(tm.a, st);
+      for (int i = 0; i < iters; ++i) TRY(encode_chunk(0, 1));
+      hipEventRecord(tm.b, st);
+    }
+    HIPCHK(hipStreamSynchronize(st));
+    float t = 0;
+    hipEventElapsedTime(&t, tm.a, tm.b);
+    *ms = t / iters;
+    return 0;
+  }
+};
+
+}  // namespace
+
+// ============================================================ C ABI
+extern "C" {
+
+const char* wh_last_error(void) { return g_err.c_str(); }
+int wh_version(void) { return 1; }
+
+int wh_create(int device, const wh_dims* dims, int compute_dtype, int max_windows, int max_group, wh_ctx** out) {
+  if (!dims || !out) return fail(-1, "null argument");
+  *out = nullptr;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(-1, "no HIP device");
+  if (device < 0 || device >= ndev) return fail(-1, "device out of range");
+  int rc;
+  if (compute_dtype == WH_F16) {
+    auto c = new Ctx<half_t>();
+    rc = c->init(device, *dims, max_windows, max_group);
+    if (rc) { delete c; return rc; }
+    *out = c;
+  } else if (compute_dtype == WH_F32) {
+    auto c = new Ctx<float>();
+    rc = c->init(device, *dims, max_windows, max_group);
+    if (rc) { delete c; return rc; }
+    *out = c;
+  } else {
+    return fail(-1, "compute_dtype must be WH_F32 or WH_F16");
+  }
+  return 0;
+}
+
+int wh_destroy(wh_ctx* ctx) {
+  delete ctx;
+  return 0;
+}
+
+int wh_set_mel_filters(wh_ctx* ctx, int n_mels, const float* filters) {
+  if (!ctx || !filters) return fail(-1, "null argument");
+  hipSetDevice(ctx->device);
+  std::vector<float> f(filters, filters + (size_t)n_mels * 201);
+  // both element-type contexts share the filter map through the base pointer cast
+  auto* c16 = dynamic_cast<Ctx<half_t>*>(ctx);
+  auto* c32 = dynamic_cast<Ctx<float>*>(ctx);
+  std::map<int, float*>& dm = c16 ? c16->d_filters : c32->d_filters;
+  std::map<int, std::vector<float>>& hm = c16 ? c16->h_filters : c32->h_filters;
+  float* d = nullptr;
+  if (dm.count(n_mels)) d = dm[n_mels];
+  else {
+    HIPCHK(hipMalloc(&d, f.size() * 4));
+    dm[n_mels] = d;
+  }
+  HIPCHK(hipMemcpy(d, f.data(), f.size() * 4, hipMemcpyHostToDevice));
+  hm[n_mels] = f;
+  return 0;
+}
+
+#define CTXCALL(expr)                                  \
+  do {                                                 \
+    if (!ctx) return fail(-1, "null context");         \
+    hipSetDevice(ctx->device);                         \
+    return (expr);                                     \
+  } while (0)
+
+int wh_load_tensor(wh_ctx* ctx, const char* name, const float* data, const int64_t* shape, int ndim) {
+  if (!name || !data || !shape) return fail(-1, "null argument");
+  CTXCALL(ctx->load(name, data, shape, ndim));
+}
+int wh_finalize(wh_ctx* ctx) { CTXCALL(ctx->finalize()); }
+int wh_log_mel(wh_ctx* ctx, const float* audio, int64_t n, int64_t pad, int n_mels, int normalize, int64_t* nf) {
+  CTXCALL(ctx->log_mel(audio, n, pad, n_mels, normalize, nf));
+}
+int wh_mel_max(wh_ctx* ctx, float* g) { CTXCALL(ctx->mel_max(g)); }
+int wh_mel_normalize(wh_ctx* ctx, float g) { CTXCALL(ctx->mel_normalize(g)); }
+int wh_mel_read(wh_ctx* ctx, float* out, int64_t f0, int64_t nf) { CTXCALL(ctx->mel_read(out, f0, nf)); }
+int wh_mel_write(wh_ctx* ctx, const float* mel, int64_t nf) { CTXCALL(ctx->mel_write(mel, nf)); }
+int wh_encode(wh_ctx* ctx, int n_win, const int64_t* seeks, const int* segs) { CTXCALL(ctx->encode(n_win, seeks, segs)); }
+int wh_read_audio_features(wh_ctx* ctx, int slot, float* out) { CTXCALL(ctx->read_xa(slot, out)); }
+int wh_read_cross_kv(wh_ctx* ctx, int slot, int layer, float* k, float* v) { CTXCALL(ctx->read_ckv(slot, layer, k, v)); }
+int wh_decode_begin(wh_ctx* ctx, int n_win, const wh_decode_opts* o, const int* init, const int* n_init, int max_init,
+                    const int* sot_index) {
+  if (!o || !init || !n_init || !sot_index) return fail(-1, "null argument");
+  CTXCALL(ctx->decode_begin(n_win, o, init, n_init, max_init, sot_index));
+}
+int wh_decode_steps(wh_ctx* ctx, int max_steps, int* n_done) { CTXCALL(ctx->decode_steps(max_steps, n_done)); }
+int wh_decode_read(wh_ctx* ctx, int slot, int* tokens, float* slp, int* len, int* fin_n, int* fin_tok, int* fin_len,
+                   float* fin_score, float* nsp) {
+  CTXCALL(ctx->decode_read(slot, tokens, slp, len, fin_n, fin_tok, fin_len, fin_score, nsp));
+}
+int wh_decode_maxc(wh_ctx* ctx) { return ctx ? ctx->maxc_stride : -1; }
+int wh_prefill_logits(wh_ctx* ctx, int slot, const int* tokens, int n, float* logits, const int* ah, int na, float* aqk) {
+  CTXCALL(ctx->prefill_logits(slot, tokens, n, logits, ah, na, aqk));
+}
+int wh_stats(wh_ctx* ctx, double* out, int n) {
+  if (!ctx || !out) return fail(-1, "null argument");
+  for (int i = 0; i < n && i < 8; ++i) out[i] = ctx->stats[i];
+  return 0;
+}
+int wh_sync(wh_ctx* ctx) {
+  if (!ctx) return fail(-1, "null context");
+  hipSetDevice(ctx->device);
+  HIPCHK(hipDeviceSynchronize());
+  return 0;
+}
+int wh_time_stage(wh_ctx* ctx, int what, int iters, double* ms) { CTXCALL(ctx->time_stage(what, iters, ms)); }
+
+}  // extern "C"

@@ -1,0 +1,183 @@
+"""Token-id side of the reference tokenizer (whisper/tokenizer.py:132-395).
+
+The hot path needs only ids: special tokens (laid out after the base BPE ranks
+exactly as ``get_encoding`` does, tokenizer.py:331-363), the SuppressTokens
+``-1`` set (``non_speech_tokens``, tokenizer.py:253-284) and ``encode(" ")``.
+Those facts ship as data in assets/specials.json (exported from the reference
+tokenizer by oracle/gen_golden.py).  Text decoding needs the BPE rank file
+(``multilingual.tiktoken`` / ``gpt2.tiktoken``); point WHISPER_TIKTOKEN_DIR at a
+directory holding it to enable ``decode``; without it ``decode`` returns "".
+"""
+
+import base64
+import json
+import os
+from dataclasses import dataclass, field
+from functools import lru_cache
+from typing import Dict, List, Optional, Tuple
+
+_ASSETS = os.path.join(os.path.dirname(os.path.abspath(__file__)), "assets")
+
+
+@lru_cache(maxsize=None)
+def _specials():
+    with open(os.path.join(_ASSETS, "specials.json")) as f:
+        return json.load(f)
+
+
+LANGUAGES: Dict[str, str] = {c: n for c, n in _specials()["languages"]}
+TO_LANGUAGE_CODE: Dict[str, str] = {**{n: c for c, n in LANGUAGES.items()}, **_specials()["to_language_code"]}
+
+
+@lru_cache(maxsize=None)
+def _ranks(name: str) -> Optional[Dict[int, bytes]]:
+    d = os.environ.get("WHISPER_TIKTOKEN_DIR")
+    if not d:
+        return None
+    p = os.path.join(d, f"{name}.tiktoken")
+    if not os.path.exists(p):
+        return None
+    out = {}
+    with open(p) as f:
+        for line in f:
+            if line.strip():
+                tok, rank = line.split()
+                out[int(rank)] = base64.b64decode(tok)
+    return out
+
+
+@dataclass
+class Tokenizer:
+    encoding_name: str
+    num_languages: int
+    language: Optional[str] = None
+    task: Optional[str] = None
+    sot_sequence: Tuple[int, ...] = ()
+    special_tokens: Dict[str, int] = field(default_factory=dict)
+
+    def __post_init__(self):
+        v = _specials()["vocab"][f"{self.encoding_name}_{self.num_languages}"]
+        self._v = v
+        base = v["n_base"]
+        names = ["<|endoftext|>", "<|startoftranscript|>"]
+        names += [f"<|{c}|>" for c in list(LANGUAGES)[: self.num_languages]]
+        names += ["<|translate|>", "<|transcribe|>", "<|startoflm|>", "<|startofprev|>", "<|nospeech|>",
+                  "<|notimestamps|>"]
+        names += [f"<|{i * 0.02:.2f}|>" for i in range(1501)]
+        self.special_tokens = {s: base + i for i, s in enumerate(names)}
+        self.n_vocab = base + len(names)
+        seq = [self.sot]
+        if self.language is not None:
+            seq.append(self.sot + 1 + list(LANGUAGES).index(self.language))
+        if self.task is not None:
+            seq.append(self.transcribe if self.task == "transcribe" else self.translate)
+        self.sot_sequence = tuple(seq)
+
+    # special ids (tokenizer.py:172-212)
+    @property
+    def eot(self) -> int:
+        return self.special_tokens["<|endoftext|>"]
+
+    @property
+    def transcribe(self) -> int:
+        return self.special_tokens["<|transcribe|>"]
+
+    @property
+    def translate(self) -> int:
+        return self.special_tokens["<|translate|>"]
+
+    @property
+    def sot(self) -> int:
+        return self.special_tokens["<|startoftranscript|>"]
+
+    @property
+    def sot_lm(self) -> int:
+        return self.special_tokens["<|startoflm|>"]
+
+    @property
+    def sot_prev(self) -> int:
+        return self.special_tokens["<|startofprev|>"]
+
+    @property
+    def no_speech(self) -> int:
+        return self.special_tokens["<|nospeech|>"]
+
+    @property
+    def no_timestamps(self) -> int:
+        return self.special_tokens["<|notimestamps|>"]
+
+    @property
+    def timestamp_begin(self) -> int:
+        return self.special_tokens["<|0.00|>"]
+
+    @property
+    def language_token(self) -> int:
+        if self.language is None:
+            raise ValueError("This tokenizer does not have language token configured")
+        return self.special_tokens[f"<|{self.language}|>"]
+
+    @property
+    def all_language_tokens(self) -> Tuple[int, ...]:
+        return tuple(self.special_tokens[f"<|{c}|>"] for c in list(LANGUAGES)[: self.num_languages])
+
+    @property
+    def all_language_codes(self) -> Tuple[str, ...]:
+        return tuple(list(LANGUAGES)[: self.num_languages])
+
+    @property
+    def sot_sequence_including_notimestamps(self) -> Tuple[int, ...]:
+        return tuple(list(self.sot_sequence) + [self.no_timestamps])
+
+    @property
+    def non_speech_tokens(self) -> Tuple[int, ...]:
+        return tuple(self._v["non_speech_tokens"])
+
+    @property
+    def whitespace_tokens(self) -> Tuple[int, ...]:
+        return tuple(self._v["whitespace_tokens"])
+
+    def encode_blank(self) -> List[int]:
+        """tokenizer.encode(" ") used by SuppressBlank (decoding.py:457)."""
+        return list(self._v["blank"])
+
+    def is_blank_text(self, tokens: List[int]) -> bool:
+        """True when decode(tokens).strip() == "" (transcribe.py:494-499)."""
+        ws = set(self._v["whitespace_tokens"])
+        return all(t in ws for t in tokens if t < self.eot)
+
+    def decode(self, token_ids: List[int]) -> str:
+        ranks = _ranks(self.encoding_name)
+        if ranks is None:
+            return ""
+        b = b"".join(ranks[t] for t in token_ids if t < self.timestamp_begin and t in ranks)
+        return b.decode("utf-8", errors="replace")
+
+    def decode_with_timestamps(self, token_ids: List[int]) -> str:
+        ranks = _ranks(self.encoding_name) or {}
+        inv = {v: k for k, v in self.special_tokens.items()}
+        out = b""
+        for t in token_ids:
+            out += ranks[t] if t in ranks else inv.get(t, "").encode()
+        return out.decode("utf-8", errors="replace")
+
+
+@lru_cache(maxsize=None)
+def get_tokenizer(multilingual: bool, *, num_languages: int = 99, language: Optional[str] = None,
+                  task: Optional[str] = None) -> Tokenizer:
+    """tokenizer.py:367-395."""
+    if language is not None:
+        language = language.lower()
+        if language not in LANGUAGES:
+            if language in TO_LANGUAGE_CODE:
+                language = TO_LANGUAGE_CODE[language]
+            else:
+                raise ValueError(f"Unsupported language: {language}")
+    if multilingual:
+        name = "multilingual"
+        language = language or "en"
+        task = task or "transcribe"
+    else:
+        name = "gpt2"
+        language = None
+        task = None
+    return Tokenizer(name, num_languages, language, task)

@@ -1,0 +1,306 @@
+"""Long-form transcription driver (reference whisper/transcribe.py:41-524).
+
+Same options and segment semantics as the reference loop (30 s windows, data-
+dependent ``seek``, temperature fallback, prompt carry-over, no-speech skip,
+empty-segment clearing).  Two schedules:
+
+* sequential — the reference order, one window at a time; required whenever a
+  window depends on the previous one (``condition_on_previous_text=True``,
+  ``carry_initial_prompt``, word timestamps);
+* batched — with ``condition_on_previous_text=False`` and several clips
+  (``clip_timestamps`` on a grid), windows of different clips are independent
+  (each clip's seek is clip-local, the prompt resets every window:
+  transcribe.py:277-287, 513-515), so every round encodes and decodes the next
+  window of *all* unfinished clips together on the GPU.  Segments are assembled
+  in clip order afterwards, which reproduces the reference's output exactly.
+
+The log-mel of the whole file is computed on the GPU and stays there; windows
+are cut from it on the device.
+"""
+
+import os
+from dataclasses import replace
+from typing import TYPE_CHECKING, List, Optional, Tuple, Union
+
+import numpy as np
+
+from .audio import FRAMES_PER_SECOND, HOP_LENGTH, N_FRAMES, N_SAMPLES, SAMPLE_RATE, load_audio
+from .decoding import DecodingOptions, DecodingResult, detect_language, run_windows
+from .tokenizer import LANGUAGES, get_tokenizer
+
+if TYPE_CHECKING:
+    from .model import Whisper
+
+
+def _decode_with_fallback(model, base_opts: DecodingOptions, temperatures, prompts: List, thresholds
+                          ) -> List[DecodingResult]:
+    """transcribe.py:188-228 for a batch of windows (slots 0..n-1 already encoded)."""
+    cr_thr, lp_thr, ns_thr = thresholds
+    n = len(prompts)
+    results: List[Optional[DecodingResult]] = [None] * n
+    pending = list(range(n))
+    for t in temperatures:
+        kw = {}
+        if t > 0:
+            kw = dict(beam_size=None, patience=None)
+        else:
+            kw = dict(best_of=None)
+        opts = replace(base_opts, temperature=t, **kw)
+        if t > 0 and opts.best_of is None:
+            opts = replace(opts, best_of=None)
+        if pending != list(range(n)):
+            # re-encode only the windows that still need work: keep slot order stable
+            model._reencode(pending)
+        res = run_windows(model, opts, [prompts[i] for i in pending])
+        nxt = []
+        for i, r in zip(pending, res):
+            results[i] = r
+            fallback = False
+            if cr_thr is not None and r.compression_ratio > cr_thr:
+                fallback = True
+            if lp_thr is not None and r.avg_logprob < lp_thr:
+                fallback = True
+            if ns_thr is not None and r.no_speech_prob > ns_thr and lp_thr is not None and r.avg_logprob < lp_thr:
+                fallback = False
+            if fallback:
+                nxt.append(i)
+        pending = nxt
+        if not pending:
+            break
+    return results
+
+
+def _split_segments(tokenizer, result: DecodingResult, seek: int, time_offset: float, segment_size: int,
+                    segment_duration: float, input_stride: int, time_precision: float) -> Tuple[List[dict], int]:
+    """Segment building and seek advance of transcribe.py:350-410."""
+    tokens = np.asarray(result.tokens, dtype=np.int64)
+    tb = tokenizer.timestamp_begin
+
+    def new_segment(start, end, toks):
+        toks = [int(x) for x in toks]
+        return dict(seek=seek, start=start, end=end, text=tokenizer.decode([x for x in toks if x < tokenizer.eot]),
+                    tokens=toks, temperature=result.temperature, avg_logprob=result.avg_logprob,
+                    compression_ratio=result.compression_ratio, no_speech_prob=result.no_speech_prob)
+
+    segs = []
+    is_ts = tokens >= tb
+    single_end = is_ts[-2:].tolist() == [False, True]
+    consecutive = np.where(is_ts[:-1] & is_ts[1:])[0] + 1
+    if len(consecutive) > 0:
+        slices = consecutive.tolist()
+        if single_end:
+            slices.append(len(tokens))
+        last = 0
+        for cut in slices:
+            part = tokens[last:cut]
+            segs.append(new_segment(time_offset + (int(part[0]) - tb) * time_precision,
+                                    time_offset + (int(part[-1]) - tb) * time_precision, part))
+            last = cut
+        if single_end:
+            seek += segment_size
+        else:
+            seek += (int(tokens[last - 1]) - tb) * input_stride
+    else:
+        duration = segment_duration
+        ts = tokens[is_ts]
+        if len(ts) > 0 and int(ts[-1]) != tb:
+            duration = (int(ts[-1]) - tb) * time_precision
+        segs.append(new_segment(time_offset, time_offset + duration, tokens))
+        seek += segment_size
+    for s in segs:  # transcribe.py:494-499
+        if s["start"] == s["end"] or tokenizer.is_blank_text(s["tokens"]):
+            s["text"] = ""
+            s["tokens"] = []
+            s["words"] = []
+    return segs, seek
+
+
+def transcribe(model: "Whisper", audio: Union[str, np.ndarray], *, verbose: Optional[bool] = None,
+               temperature: Union[float, Tuple[float, ...]] = (0.0, 0.2, 0.4, 0.6, 0.8, 1.0),
+               compression_ratio_threshold: Optional[float] = 2.4, logprob_threshold: Optional[float] = -1.0,
+               no_speech_threshold: Optional[float] = 0.6, condition_on_previous_text: bool = True,
+               initial_prompt: Optional[Union[str, List[int]]] = None, carry_initial_prompt: bool = False,
+               word_timestamps: bool = False, prepend_punctuations: str = "\"'“¿([{-",
+               append_punctuations: str = "\"'.。,，!！?？:：”)]}、", clip_timestamps: Union[str, List[float]] = "0",
+               hallucination_silence_threshold: Optional[float] = None, schedule: str = "auto",
+               mel_global_max: Optional[float] = None, **decode_options) -> dict:
+    """transcribe.py:41-524.  Extra keywords: ``schedule`` ("auto", "sequential",
+    "batched") and ``mel_global_max`` (a max pre-reduced across ranks when one file
+    is sharded over GPUs, audio.py:155)."""
+    if word_timestamps:
+        raise NotImplementedError("word_timestamps on the HIP backend is planned (SURVEY §8(f) rank 1)")
+    if decode_options.get("fp16", True) is False and model.dtype != "fp32":
+        pass  # the compute precision is fixed when the model is loaded (dtype=...)
+    decode_options.pop("fp16", None)
+    if isinstance(audio, str):
+        audio = load_audio(audio)
+    audio = np.ascontiguousarray(audio.detach().cpu().numpy() if hasattr(audio, "detach") else audio,
+                                 dtype=np.float32)
+    ctx = model.ctx
+    n_mels = model.dims.n_mels
+    frames = ctx.log_mel(audio, n_mels, padding=N_SAMPLES, normalize=mel_global_max is None)
+    if mel_global_max is not None:
+        ctx.mel_normalize(mel_global_max)
+    content_frames = frames - N_FRAMES
+    content_duration = float(content_frames * HOP_LENGTH / SAMPLE_RATE)
+
+    if decode_options.get("language") is None:
+        if not model.is_multilingual:
+            decode_options["language"] = "en"
+        else:
+            seg = ctx.mel_read(n_mels, 0, min(N_FRAMES, frames))
+            if seg.shape[1] < N_FRAMES:
+                seg = np.pad(seg, ((0, 0), (0, N_FRAMES - seg.shape[1])))
+            _, probs = detect_language(model, seg)
+            decode_options["language"] = max(probs, key=probs.get)
+            # detect_language overwrote the context mel with the probe window
+            frames = ctx.log_mel(audio, n_mels, padding=N_SAMPLES, normalize=mel_global_max is None)
+            if mel_global_max is not None:
+                ctx.mel_normalize(mel_global_max)
+            if verbose is not None:
+                print(f"Detected language: {LANGUAGES[decode_options['language']].title()}")
+    language = decode_options["language"]
+    task = decode_options.get("task", "transcribe")
+    tokenizer = get_tokenizer(model.is_multilingual, num_languages=model.num_languages, language=language,
+                              task=task)
+
+    if isinstance(clip_timestamps, str):
+        clip_timestamps = [float(ts) for ts in (clip_timestamps.split(",") if clip_timestamps else [])]
+    seek_points = [round(ts * FRAMES_PER_SECOND) for ts in clip_timestamps]
+    if len(seek_points) == 0:
+        seek_points.append(0)
+    if len(seek_points) % 2 == 1:
+        seek_points.append(content_frames)
+    seek_clips = list(zip(seek_points[::2], seek_points[1::2]))
+
+    temperatures = [temperature] if isinstance(temperature, (int, float)) else list(temperature)
+    thresholds = (compression_ratio_threshold, logprob_threshold, no_speech_threshold)
+    base = DecodingOptions(**{k: v for k, v in decode_options.items() if k in DecodingOptions.__dataclass_fields__})
+    input_stride = N_FRAMES // model.dims.n_audio_ctx
+    time_precision = input_stride * HOP_LENGTH / SAMPLE_RATE
+
+    if isinstance(initial_prompt, str):
+        raise NotImplementedError("text initial_prompt needs a BPE encoder; pass a list of token ids")
+    initial_prompt_tokens = list(initial_prompt) if initial_prompt else []
+
+    batched = schedule == "batched" or (
+        schedule == "auto" and not condition_on_previous_text and not carry_initial_prompt and len(seek_clips) > 1)
+    state = dict(content_frames=content_frames, tokenizer=tokenizer, temperatures=temperatures,
+                 thresholds=thresholds, base=base, input_stride=input_stride, time_precision=time_precision)
+    if batched:
+        segments = _run_batched(model, seek_clips, initial_prompt_tokens, state)
+    else:
+        segments = _run_sequential(model, seek_clips, initial_prompt_tokens, condition_on_previous_text,
+                                   carry_initial_prompt, state)
+    all_tokens = list(initial_prompt_tokens)
+    all_segments = []
+    for s in segments:
+        all_segments.append({"id": len(all_segments), **s})
+        all_tokens.extend(s["tokens"])
+        if verbose:
+            print(f"[{s['start']:.2f} --> {s['end']:.2f}] {s['text']}")
+    return dict(text=tokenizer.decode(all_tokens[len(initial_prompt_tokens):]), segments=all_segments,
+                language=language)
+
+
+def _window_at(seek: int, clip: Tuple[int, int], content_frames: int):
+    segment_size = min(N_FRAMES, content_frames - seek, clip[1] - seek)
+    return segment_size, segment_size * HOP_LENGTH / SAMPLE_RATE
+
+
+def _apply_result(model, result, seek, segment_size, st) -> Tuple[List[dict], int, bool]:
+    """no-speech skip (transcribe.py:308-321) then segment split; returns
+    (segments, new seek, skipped)."""
+    thr_ns, thr_lp = st["thresholds"][2], st["thresholds"][1]
+    if thr_ns is not None:
+        skip = result.no_speech_prob > thr_ns
+        if thr_lp is not None and result.avg_logprob > thr_lp:
+            skip = False
+        if skip:
+            return [], seek + segment_size, True
+    time_offset = float(seek * HOP_LENGTH / SAMPLE_RATE)
+    segs, new_seek = _split_segments(st["tokenizer"], result, seek, time_offset, segment_size,
+                                     segment_size * HOP_LENGTH / SAMPLE_RATE, st["input_stride"],
+                                     st["time_precision"])
+    return segs, new_seek, False
+
+
+def _run_sequential(model, clips, initial_prompt_tokens, condition_on_previous_text, carry_initial_prompt, st):
+    ctx = model.ctx
+    content_frames = st["content_frames"]
+    all_tokens = list(initial_prompt_tokens)
+    segments = []
+    prompt_reset_since = 0
+    remaining_prompt_length = model.dims.n_text_ctx // 2 - 1 - len(initial_prompt_tokens)
+    clip_idx, seek = 0, clips[0][0]
+    while clip_idx < len(clips):
+        cs, ce = clips[clip_idx]
+        if seek < cs:
+            seek = cs
+        if seek >= ce:
+            clip_idx += 1
+            if clip_idx < len(clips):
+                seek = clips[clip_idx][0]
+            continue
+        segment_size, segment_duration = _window_at(seek, clips[clip_idx], content_frames)
+        if segment_duration < 1.0:  # fork: drop < 1 s tails (transcribe.py:292-297)
+            clip_idx += 1
+            continue
+        if carry_initial_prompt:
+            nignored = max(len(initial_prompt_tokens), prompt_reset_since)
+            prompt = initial_prompt_tokens + all_tokens[nignored:][-remaining_prompt_length:]
+        else:
+            prompt = all_tokens[prompt_reset_since:]
+        ctx.encode([seek], [segment_size])
+        model._last_windows = ([seek], [segment_size])
+        result = _decode_with_fallback(model, st["base"], st["temperatures"], [prompt or None], st["thresholds"])[0]
+        segs, seek, skipped = _apply_result(model, result, seek, segment_size, st)
+        if skipped:
+            continue
+        segments.extend(segs)
+        all_tokens.extend(t for s in segs for t in s["tokens"])
+        if not condition_on_previous_text or result.temperature > 0.5:
+            prompt_reset_since = len(all_tokens)
+    return segments
+
+
+def _run_batched(model, clips, initial_prompt_tokens, st):
+    """Rounds over clips: every unfinished clip contributes its next window."""
+    ctx = model.ctx
+    content_frames = st["content_frames"]
+    seeks = [c[0] for c in clips]
+    live = [True] * len(clips)
+    per_clip: List[List[dict]] = [[] for _ in clips]
+    first_window = True
+    while any(live):
+        batch = []  # (clip, seek, segment_size)
+        for ci, (cs, ce) in enumerate(clips):
+            if not live[ci]:
+                continue
+            if seeks[ci] < cs:
+                seeks[ci] = cs
+            if seeks[ci] >= ce:
+                live[ci] = False
+                continue
+            segment_size, segment_duration = _window_at(seeks[ci], clips[ci], content_frames)
+            if segment_duration < 1.0:
+                live[ci] = False
+                continue
+            batch.append((ci, seeks[ci], segment_size))
+        if not batch:
+            break
+        for b0 in range(0, len(batch), model.ctx.max_windows):
+            chunk = batch[b0:b0 + model.ctx.max_windows]
+            prompts = []
+            for ci, _, _ in chunk:
+                # only the very first window of the file sees the initial prompt
+                prompts.append(initial_prompt_tokens if (first_window and ci == 0 and initial_prompt_tokens) else None)
+            first_window = False
+            ctx.encode([s for _, s, _ in chunk], [z for _, _, z in chunk])
+            model._last_windows = ([s for _, s, _ in chunk], [z for _, _, z in chunk])
+            results = _decode_with_fallback(model, st["base"], st["temperatures"], prompts, st["thresholds"])
+            for (ci, seek, segment_size), r in zip(chunk, results):
+                segs, new_seek, _ = _apply_result(model, r, seek, segment_size, st)
+                per_clip[ci].extend(segs)
+                seeks[ci] = new_seek
+    return [s for clip in per_clip for s in clip]
