@@ -82,6 +82,8 @@ int wh_set_mel_filters(wh_ctx* ctx, int n_mels, const float* filters);
    normalize = 1 applies the global-max floor and scaling immediately. */
 int wh_log_mel(wh_ctx* ctx, const float* audio, int64_t n_samples, int64_t padding, int n_mels, int normalize,
                int64_t* n_frames);
+/* keep audio resident in HBM; wh_log_mel(ctx, NULL, n, ...) then computes from it */
+int wh_audio_upload(wh_ctx* ctx, const float* audio, int64_t n_samples);
 int wh_mel_max(wh_ctx* ctx, float* gmax);              /* raw log10 max of the last wh_log_mel */
 int wh_mel_normalize(wh_ctx* ctx, float gmax);         /* floor at gmax-8, (x+4)/4 */
 int wh_mel_read(wh_ctx* ctx, float* out, int64_t frame0, int64_t n_frames); /* [n_mels][n_frames] */

@@ -123,7 +123,7 @@ def model_goldens(name: str, seed: int = 0, audio_seed: int = 1, full: bool = Fa
         # ck: (L, H, 64, 1500); cv: (L, H, 1500, 64)
         out["ck_norm"] = ck.double().norm(dim=(2, 3)).numpy()
         out["cv_norm"] = cv.double().norm(dim=(2, 3)).numpy()
-        out["ck_slice"] = ck[:, :, :, :32].numpy().astype(np.float32)
+        out["ck_slice"] = (ck[:, :, :, :32] if full else ck[[0, -1]][:, :, :, :8]).numpy().astype(np.float32)
         tok = refw.tokenizer.get_tokenizer(model.is_multilingual, num_languages=model.num_languages,
                                            language="en", task="transcribe")
         sot = list(tok.sot_sequence)

@@ -88,6 +88,7 @@ struct wh_ctx {
   virtual int load(const std::string& name, const float* data, const int64_t* shape, int ndim) = 0;
   virtual int finalize() = 0;
   virtual int log_mel(const float* audio, int64_t n, int64_t pad, int n_mels, int normalize, int64_t* nf) = 0;
+  virtual int audio_upload(const float* audio, int64_t n) = 0;
   virtual int mel_max(float* g) = 0;
   virtual int mel_normalize(float g) = 0;
   virtual int mel_read(float* out, int64_t f0, int64_t nf) = 0;
@@ -446,11 +447,25 @@ struct Ctx : public wh_ctx {
   }
 
   // ------------------------------------------------------------ mel
+  int64_t audio_n = 0;
+  int audio_upload(const float* audio, int64_t n) override {
+    if ((size_t)n > audio_cap) {
+      if (d_audio) hipFree(d_audio);
+      audio_cap = std::max<size_t>(n, 16000);
+      HIPCHK(hipMalloc(&d_audio, audio_cap * 4));
+    }
+    HIPCHK(hipMemcpyAsync(d_audio, audio, n * 4, hipMemcpyHostToDevice, st));
+    HIPCHK(hipStreamSynchronize(st));
+    audio_n = n;
+    return 0;
+  }
+  // audio == nullptr: use the resident buffer of wh_audio_upload (n must match)
   int log_mel(const float* audio, int64_t n, int64_t pad, int n_mels, int normalize, int64_t* nf) override {
     if (!h_filters.count(n_mels)) return fail(-7, "mel filters for n_mels=" + std::to_string(n_mels) + " not set");
     if (n + pad <= 200) return fail(-7, "audio too short for reflect padding");
+    if (!audio && n != audio_n) return fail(-7, "no resident audio of that length");
     const int64_t frames = (n + pad) / 160;
-    if ((size_t)n > audio_cap) {
+    if (audio && (size_t)n > audio_cap) {
       if (d_audio) hipFree(d_audio);
       audio_cap = std::max<size_t>(n, 16000);
       HIPCHK(hipMalloc(&d_audio, audio_cap * 4));
@@ -462,7 +477,10 @@ struct Ctx : public wh_ctx {
       HIPCHK(hipMalloc(&d_mel, mel_cap * 4));
     }
     hipEventRecord(tm.a, st);
-    HIPCHK(hipMemcpyAsync(d_audio, audio, n * 4, hipMemcpyHostToDevice, st));
+    if (audio) {
+      HIPCHK(hipMemcpyAsync(d_audio, audio, n * 4, hipMemcpyHostToDevice, st));
+      audio_n = n;
+    }
     HIPCHK(hipMemsetAsync(d_gmax, 0, 16, st));
     launch_mel(d_audio, n, n + pad, 0, frames, d_filters[n_mels], n_mels, d_mel, frames, d_gmax, st);
     if (normalize) launch_mel_norm(d_mel, frames, frames, n_mels, d_gmax, nullptr, st);
@@ -993,6 +1011,10 @@ int wh_load_tensor(wh_ctx* ctx, const char* name, const float* data, const int64
 int wh_finalize(wh_ctx* ctx) { CTXCALL(ctx->finalize()); }
 int wh_log_mel(wh_ctx* ctx, const float* audio, int64_t n, int64_t pad, int n_mels, int normalize, int64_t* nf) {
   CTXCALL(ctx->log_mel(audio, n, pad, n_mels, normalize, nf));
+}
+int wh_audio_upload(wh_ctx* ctx, const float* audio, int64_t n) {
+  if (!audio || n <= 0) return fail(-1, "bad audio");
+  CTXCALL(ctx->audio_upload(audio, n));
 }
 int wh_mel_max(wh_ctx* ctx, float* g) { CTXCALL(ctx->mel_max(g)); }
 int wh_mel_normalize(wh_ctx* ctx, float g) { CTXCALL(ctx->mel_normalize(g)); }

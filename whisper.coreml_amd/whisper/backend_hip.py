@@ -51,6 +51,7 @@ _EXPORTS = {
     "wh_finalize": (c_int, [c_void_p]),
     "wh_set_mel_filters": (c_int, [c_void_p, c_int, c_void_p]),
     "wh_log_mel": (c_int, [c_void_p, c_void_p, c_int64, c_int64, c_int, c_int, POINTER(c_int64)]),
+    "wh_audio_upload": (c_int, [c_void_p, c_void_p, c_int64]),
     "wh_mel_max": (c_int, [c_void_p, POINTER(c_float)]),
     "wh_mel_normalize": (c_int, [c_void_p, c_float]),
     "wh_mel_read": (c_int, [c_void_p, c_void_p, c_int64, c_int64]),
@@ -94,6 +95,15 @@ def load_library(path: Optional[str] = None):
 
 def _ptr(a: np.ndarray):
     return a.ctypes.data_as(c_void_p)
+
+
+class DeviceAudio:
+    """Audio already resident in a context's HBM (``HipContext.audio_upload``);
+    ``transcribe`` then starts from device memory (no host-to-device copy)."""
+
+    def __init__(self, ctx, n_samples: int):
+        self.ctx = ctx
+        self.n_samples = n_samples
 
 
 class HipContext:
@@ -149,6 +159,17 @@ class HipContext:
         a = np.ascontiguousarray(audio, dtype=np.float32)
         nf = c_int64()
         self._check(self.lib.wh_log_mel(self.h, _ptr(a), a.shape[0], int(padding), n_mels, int(normalize),
+                                        ctypes.byref(nf)), "wh_log_mel")
+        return nf.value
+
+    def audio_upload(self, audio: np.ndarray) -> "DeviceAudio":
+        a = np.ascontiguousarray(audio, dtype=np.float32)
+        self._check(self.lib.wh_audio_upload(self.h, _ptr(a), a.shape[0]), "wh_audio_upload")
+        return DeviceAudio(self, a.shape[0])
+
+    def log_mel_resident(self, n_samples: int, n_mels: int, padding: int = 0, normalize: bool = True) -> int:
+        nf = c_int64()
+        self._check(self.lib.wh_log_mel(self.h, None, n_samples, int(padding), n_mels, int(normalize),
                                         ctypes.byref(nf)), "wh_log_mel")
         return nf.value
 

@@ -25,6 +25,7 @@ from typing import TYPE_CHECKING, List, Optional, Tuple, Union
 import numpy as np
 
 from .audio import FRAMES_PER_SECOND, HOP_LENGTH, N_FRAMES, N_SAMPLES, SAMPLE_RATE, load_audio
+from .backend_hip import DeviceAudio
 from .decoding import DecodingOptions, DecodingResult, detect_language, run_windows
 from .tokenizer import LANGUAGES, get_tokenizer
 
@@ -123,24 +124,41 @@ def transcribe(model: "Whisper", audio: Union[str, np.ndarray], *, verbose: Opti
                word_timestamps: bool = False, prepend_punctuations: str = "\"'“¿([{-",
                append_punctuations: str = "\"'.。,，!！?？:：”)]}、", clip_timestamps: Union[str, List[float]] = "0",
                hallucination_silence_threshold: Optional[float] = None, schedule: str = "auto",
-               mel_global_max: Optional[float] = None, **decode_options) -> dict:
+               mel_max_reduce=None, **decode_options) -> dict:
     """transcribe.py:41-524.  Extra keywords: ``schedule`` ("auto", "sequential",
-    "batched") and ``mel_global_max`` (a max pre-reduced across ranks when one file
-    is sharded over GPUs, audio.py:155)."""
+    "batched") and ``mel_max_reduce`` (callable local max -> global max, used when
+    one file is sharded over GPUs: the log-mel floor is a whole-file max,
+    audio.py:155, so ranks all-reduce it before normalizing)."""
     if word_timestamps:
         raise NotImplementedError("word_timestamps on the HIP backend is planned (SURVEY §8(f) rank 1)")
     if decode_options.get("fp16", True) is False and model.dtype != "fp32":
         pass  # the compute precision is fixed when the model is loaded (dtype=...)
     decode_options.pop("fp16", None)
-    if isinstance(audio, str):
-        audio = load_audio(audio)
-    audio = np.ascontiguousarray(audio.detach().cpu().numpy() if hasattr(audio, "detach") else audio,
-                                 dtype=np.float32)
     ctx = model.ctx
     n_mels = model.dims.n_mels
-    frames = ctx.log_mel(audio, n_mels, padding=N_SAMPLES, normalize=mel_global_max is None)
-    if mel_global_max is not None:
-        ctx.mel_normalize(mel_global_max)
+    if isinstance(audio, DeviceAudio):
+        if audio.ctx is not ctx:
+            raise ValueError("DeviceAudio belongs to another model context")
+        resident = audio.n_samples
+
+        def compute_mel():
+            return ctx.log_mel_resident(resident, n_mels, padding=N_SAMPLES, normalize=mel_max_reduce is None)
+    else:
+        if isinstance(audio, str):
+            audio = load_audio(audio)
+        audio = np.ascontiguousarray(audio.detach().cpu().numpy() if hasattr(audio, "detach") else audio,
+                                     dtype=np.float32)
+
+        def compute_mel():
+            return ctx.log_mel(audio, n_mels, padding=N_SAMPLES, normalize=mel_max_reduce is None)
+
+    def prepare_mel():
+        nf = compute_mel()
+        if mel_max_reduce is not None:
+            ctx.mel_normalize(float(mel_max_reduce(ctx.mel_max())))
+        return nf
+
+    frames = prepare_mel()
     content_frames = frames - N_FRAMES
     content_duration = float(content_frames * HOP_LENGTH / SAMPLE_RATE)
 
@@ -154,9 +172,7 @@ def transcribe(model: "Whisper", audio: Union[str, np.ndarray], *, verbose: Opti
             _, probs = detect_language(model, seg)
             decode_options["language"] = max(probs, key=probs.get)
             # detect_language overwrote the context mel with the probe window
-            frames = ctx.log_mel(audio, n_mels, padding=N_SAMPLES, normalize=mel_global_max is None)
-            if mel_global_max is not None:
-                ctx.mel_normalize(mel_global_max)
+            frames = prepare_mel()
             if verbose is not None:
                 print(f"Detected language: {LANGUAGES[decode_options['language']].title()}")
     language = decode_options["language"]
