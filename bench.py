@@ -141,7 +141,8 @@ def main():
         del sd
         sd = None
     n_clips = int(round(args.seconds / 30.0))
-    clip_ts = ",".join(str(30 * i) for i in range(n_clips + 1))
+    # start,end pairs of a 30 s grid covering the whole shard (transcribe.py:172-181)
+    clip_ts = ",".join(f"{30 * i},{30 * (i + 1)}" for i in range(n_clips))
     # the rank's shard of one long synthetic file (seeded per rank)
     audio = S.synthetic_audio(args.seconds, seed=1000 + rank)
     dev_audio = model.ctx.audio_upload(audio)

@@ -40,6 +40,16 @@ WH_DEV void frag_load(Frag<float>& f, const float* p) {
   f.v = (float8_t){a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
 }
 
+// two groups of 4 consecutive elements (8 B each for half, 16 B for float)
+WH_DEV void load4x2(Frag<half_t>& f, const half_t* p0, const half_t* p1) {
+  const half4_t a = *reinterpret_cast<const half4_t*>(p0), b = *reinterpret_cast<const half4_t*>(p1);
+  f.v = (half8_t){a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+}
+WH_DEV void load4x2(Frag<float>& f, const float* p0, const float* p1) {
+  const float4_t a = *reinterpret_cast<const float4_t*>(p0), b = *reinterpret_cast<const float4_t*>(p1);
+  f.v = (float8_t){a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+}
+
 WH_DEV void mfma_step(float4_t& acc, const Frag<half_t>& a, const Frag<half_t>& b) {
   acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(a.v, b.v, acc, 0, 0, 0);
 }

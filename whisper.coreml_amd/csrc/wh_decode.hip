@@ -13,7 +13,6 @@
 namespace wh {
 
 constexpr int LR_THREADS = 1024;
-constexpr int LR_NPT = 56;  // values per thread: V <= 57344
 constexpr int KC = 9;       // candidates kept per row (beam + 1 <= 9)
 
 struct BlockRed {
@@ -110,103 +109,79 @@ __global__ __launch_bounds__(LR_THREADS) void k_logit_rows(const float* __restri
     }
   }
   const float* row = logits + (int64_t)r * ldl;
-  float x[LR_NPT];
-#pragma unroll
-  for (int k = 0; k < LR_NPT; ++k) {
-    const int i = tid + LR_THREADS * k;
-    float v = -INFINITY;
-    if (i < V) {
-      v = row[i];
-      bool kill = false;
-      if (first && o.suppress_blank)
-        for (int b = 0; b < o.n_blank; ++b) kill |= (i == o.blank[b]);
-      if (o.suppress && ((o.suppress[i >> 5] >> (i & 31)) & 1u)) kill = true;
-      if (o.timestamps) {
-        kill |= (i == o.no_ts);
-        for (int q = 0; q < nm; ++q) kill |= (i >= mlo[q] && i < mhi[q]);
-      }
-      if (kill) v = -INFINITY;
+  const bool sb_first = first && o.suppress_blank;
+  // filtered logit i (re-read from L2 on every pass: the row does not fit registers)
+  auto val = [&](int i) -> float {
+    float v = row[i];
+    bool kill = false;
+    if (sb_first)
+      for (int b = 0; b < o.n_blank; ++b) kill |= (i == o.blank[b]);
+    if (o.suppress && ((o.suppress[i >> 5] >> (i & 31)) & 1u)) kill = true;
+    if (o.timestamps) {
+      kill |= (i == o.no_ts);
+      for (int q = 0; q < nm; ++q) kill |= (i >= mlo[q] && i < mhi[q]);
     }
-    x[k] = v;
-  }
+    return kill ? -INFINITY : v;
+  };
+  bool text_killed = false;
   if (o.timestamps) {
     // ApplyTimestampRules tail: if logsumexp(logprobs[tb:]) > max(logprobs[:tb]) mask text
     float m = -INFINITY;
-#pragma unroll
-    for (int k = 0; k < LR_NPT; ++k) m = fmaxf(m, x[k]);
+    for (int i = tid; i < V; i += LR_THREADS) m = fmaxf(m, val(i));
     m = block_max(m, sm);
     float se = 0.f;
-#pragma unroll
-    for (int k = 0; k < LR_NPT; ++k) se += __expf(x[k] - m);
+    for (int i = tid; i < V; i += LR_THREADS) se += __expf(val(i) - m);
     const float lS0 = logf(block_sum(se, sm));
     float mts = -INFINITY, mtx = -INFINITY;
-#pragma unroll
-    for (int k = 0; k < LR_NPT; ++k) {
-      const int i = tid + LR_THREADS * k;
-      const float lp = (x[k] - m) - lS0;
-      if (i >= tb && i < V) mts = fmaxf(mts, lp);
-      if (i < tb) mtx = fmaxf(mtx, lp);
+    for (int i = tid; i < V; i += LR_THREADS) {
+      const float lp = (val(i) - m) - lS0;
+      if (i >= tb) mts = fmaxf(mts, lp);
+      else mtx = fmaxf(mtx, lp);
     }
     mts = block_max(mts, sm);
     mtx = block_max(mtx, sm);
     float st = 0.f;
-    if (mts > -INFINITY) {
-#pragma unroll
-      for (int k = 0; k < LR_NPT; ++k) {
-        const int i = tid + LR_THREADS * k;
-        if (i >= tb && i < V) st += __expf(((x[k] - m) - lS0) - mts);
-      }
-    }
+    if (mts > -INFINITY)
+      for (int i = tb + tid; i < V; i += LR_THREADS) st += __expf(((val(i) - m) - lS0) - mts);
     st = block_sum(st, sm);
     const float ts_lp = mts > -INFINITY ? mts + logf(st) : -INFINITY;
-    if (ts_lp > mtx) {
-#pragma unroll
-      for (int k = 0; k < LR_NPT; ++k)
-        if (tid + LR_THREADS * k < tb) x[k] = -INFINITY;
-    }
+    text_killed = ts_lp > mtx;
   }
+  auto fval = [&](int i) -> float { return (text_killed && i < tb) ? -INFINITY : val(i); };
   // final log_softmax
   float m = -INFINITY;
-#pragma unroll
-  for (int k = 0; k < LR_NPT; ++k) m = fmaxf(m, x[k]);
+  for (int i = tid; i < V; i += LR_THREADS) m = fmaxf(m, fval(i));
   m = block_max(m, sm);
   float se = 0.f;
-#pragma unroll
-  for (int k = 0; k < LR_NPT; ++k) se += __expf(x[k] - m);
+  for (int i = tid; i < V; i += LR_THREADS) se += __expf(fval(i) - m);
   const float logS = logf(block_sum(se, sm));
   float* cv = s.cand_val + (int64_t)r * KC;
   int* ci = s.cand_idx + (int64_t)r * KC;
   if (!o.beam) {
-    float bv = -INFINITY;
+    float bv = -INFINITY, bx = -INFINITY;
     int bi = 0x7fffffff;
     if (o.temperature > 0.f) {
       const unsigned long long key = splitmix64(o.seed ^ ((unsigned long long)r << 40) ^ ((unsigned long long)len << 20));
-#pragma unroll
-      for (int k = 0; k < LR_NPT; ++k) {
-        const int i = tid + LR_THREADS * k;
-        if (i >= V || x[k] == -INFINITY) continue;
+      for (int i = tid; i < V; i += LR_THREADS) {
+        const float xv = fval(i);
+        if (xv == -INFINITY) continue;
         const unsigned long long z = splitmix64(key + (unsigned long long)i);
         const float u = ((float)(z >> 40) + 0.5f) * (1.0f / 16777216.0f);
-        const float gsc = x[k] / o.temperature - logf(-logf(u));
-        if (better(gsc, i, bv, bi)) { bv = gsc; bi = i; }
+        const float gsc = xv / o.temperature - logf(-logf(u));
+        if (better(gsc, i, bv, bi)) { bv = gsc; bi = i; bx = xv; }
       }
     } else {
-#pragma unroll
-      for (int k = 0; k < LR_NPT; ++k) {
-        const int i = tid + LR_THREADS * k;
-        if (i < V && better(x[k], i, bv, bi)) { bv = x[k]; bi = i; }
+      for (int i = tid; i < V; i += LR_THREADS) {
+        const float xv = fval(i);
+        if (better(xv, i, bv, bi)) { bv = xv; bi = i; bx = xv; }
       }
     }
+    const int mine = bi;
     block_argbest(bv, bi, sm);
     // logprob of the chosen token: log_softmax(logits)[tok] (decoding.py:312-313)
-    if (tid == bi % LR_THREADS) {
-      const int kk = bi / LR_THREADS;
-      float xv = -INFINITY;
-#pragma unroll
-      for (int k = 0; k < LR_NPT; ++k)
-        if (k == kk) xv = x[k];
+    if (mine == bi && bi != 0x7fffffff) {
       ci[0] = bi;
-      cv[0] = (xv - m) - logS;
+      cv[0] = (bx - m) - logS;
     }
     return;
   }
@@ -216,11 +191,8 @@ __global__ __launch_bounds__(LR_THREADS) void k_logit_rows(const float* __restri
   int li[KC];
 #pragma unroll
   for (int q = 0; q < KC; ++q) { lv[q] = -INFINITY; li[q] = 0x7fffffff; }
-#pragma unroll
-  for (int k = 0; k < LR_NPT; ++k) {
-    const int i = tid + LR_THREADS * k;
-    if (i >= V) continue;
-    float v = x[k];
+  for (int i = tid; i < V; i += LR_THREADS) {
+    float v = fval(i);
     int vi = i;
 #pragma unroll
     for (int q = 0; q < KC; ++q) {
@@ -240,7 +212,7 @@ __global__ __launch_bounds__(LR_THREADS) void k_logit_rows(const float* __restri
     float bv = hv;
     int bi = hi;
     block_argbest(bv, bi, sm);
-    if (bi == hi && hv == bv && bi != 0x7fffffff) ++head;
+    if (bi == hi && bi != 0x7fffffff) ++head;
     if (tid == 0) {
       cv[q] = (bv - m) - logS;
       ci[q] = bi;

@@ -9,9 +9,10 @@ enum Epi {
   EPI_STORE_GELU = 1,  // out[T]  = gelu(acc + bias)
   EPI_RESID = 2,       // out_f32 += acc + bias            (residual stream, in place)
   EPI_GELU_POS = 3,    // out_f32  = gelu(acc + bias) + pos[row-in-group]   (conv2 -> x)
-  EPI_HEADSPLIT = 4,   // cross-KV: out[(l2, win, head, t, d)] = acc + bias
+  EPI_HEADSPLIT = 4,   // cross-KV: K -> [l2][win][head][t][d], V -> [l2][win][head][d][t]
   EPI_QKV_DEC = 5,     // decoder q -> out[T]; k,v -> self-KV cache at (win, slot, head, pos)
   EPI_F32_COLS = 6,    // logits: out_f32[m][n] (ragged N)
+  EPI_PARTIAL = 7,     // split-K partial: out_f32[z][m][n] (no bias; summed by k_resid_ln)
 };
 
 struct GemmArgs {
@@ -38,6 +39,9 @@ struct GemmArgs {
   void* kc = nullptr;
   void* vc = nullptr;
   int kv_beams = 0, kv_ctx = 0;
+  // skinny GEMM only: row gather (X row of output row m = x_rows[m]) and split-K
+  const int* x_rows = nullptr;
+  int ksplit = 1;
 };
 
 template <typename T, int EPI>
@@ -59,9 +63,20 @@ WH_DEV void epilogue_store(const GemmArgs& a, int m, int gi, int ri, int n, floa
     float* o = a.out_f32 + (int64_t)m * a.ldo + n;
     store4(o, gelu_f(v[0]) + p[0], gelu_f(v[1]) + p[1], gelu_f(v[2]) + p[2], gelu_f(v[3]) + p[3]);
   } else if constexpr (EPI == EPI_HEADSPLIT) {
+    // l2 even: K -> [l2][slot][h][t][64]; l2 odd: V transposed -> [l2][slot][h][64][perm(t)]
+    // blocks padded to hs_T = TKP keys; perm: within each 32-key group, key 16*hi+4*g+j
+    // moves to 8*g+4*hi+j so a lane's 8 P.V keys are contiguous (k_cross_attn)
     const int l2 = n / a.hs_state, c = n - l2 * a.hs_state, h = c >> 6, d = c & 63;
-    const int64_t idx = ((((int64_t)l2 * a.hs_nslots + a.hs_slot0 + gi) * a.hs_heads + h) * a.hs_T + ri) * 64 + d;
-    store4(reinterpret_cast<T*>(a.out) + idx, v[0], v[1], v[2], v[3]);
+    const int64_t blk = (((int64_t)l2 * a.hs_nslots + a.hs_slot0 + gi) * a.hs_heads + h) * a.hs_T * 64;
+    T* o = reinterpret_cast<T*>(a.out) + blk;
+    if ((l2 & 1) == 0) {
+      store4(o + (int64_t)ri * 64 + d, v[0], v[1], v[2], v[3]);
+    } else {
+      const int q = ri & 31;
+      const int pt = (ri & ~31) + 8 * ((q & 15) >> 2) + 4 * (q >> 4) + (q & 3);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) o[(int64_t)(d + j) * a.hs_T + pt] = from_f32<T>(v[j]);
+    }
   } else if constexpr (EPI == EPI_QKV_DEC) {
     const int ns = a.hs_state;
     if (n < ns) {
@@ -79,5 +94,8 @@ WH_DEV void epilogue_store(const GemmArgs& a, int m, int gi, int ri, int n, floa
 
 template <typename T>
 int launch_gemm(const GemmArgs& a, int epi, hipStream_t st);
+
+// split-K factor the skinny paths use for EPI_PARTIAL at this shape (<= 16)
+int gemv_ksplit(int M, int N, int K);
 
 }  // namespace wh

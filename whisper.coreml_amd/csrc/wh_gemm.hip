@@ -126,10 +126,16 @@ __global__ __launch_bounds__(256, 2) void k_gemm_tile(GemmArgs a) {
 }
 
 // ============================================================ skinny weight-streaming GEMM
-// grid: (ceil(N/16), ceil(M/(16*MT))), block 512 (8 waves split K in 32-wide steps)
+// grid: (ceil(N/16), ceil(M/(16*MT)), ksplit), block 512 = 8 waves.  The block's k-range
+// is cut in 32-wide steps dealt round-robin to the 8 waves; per batch of U steps a wave
+// issues all its W (HBM) and X (L2) fragment loads before the first MFMA (clamped
+// addresses, predicated MFMAs: no branches around loads), then the 8 waves' partial
+// tiles are summed in LDS in a fixed order.
 template <typename T, int MT, int EPI>
 __global__ __launch_bounds__(512) void k_gemv_rows(GemmArgs a) {
-  __shared__ float red[8][MT][64][4];
+  constexpr int NW = 8;
+  constexpr int U = sizeof(T) == 2 ? 4 : 2;
+  __shared__ float red[NW][MT][64][4];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int r = lane & 15, g = lane >> 4;
   const int n0 = blockIdx.x * 16;
@@ -137,57 +143,54 @@ __global__ __launch_bounds__(512) void k_gemv_rows(GemmArgs a) {
   const T* X = reinterpret_cast<const T*>(a.X);
   const T* W = reinterpret_cast<const T*>(a.W);
 
+  // split-K: blockIdx.z owns k in [kz*Kc, (kz+1)*Kc)
+  const int kz = blockIdx.z;
+  const int Kc = a.K / gridDim.z;
   int nrow = n0 + r;
   if (nrow >= a.N) nrow = a.N - 1;
-  const T* wp = W + (int64_t)nrow * a.K + 8 * g;
+  const T* wp = W + (int64_t)nrow * a.K + (int64_t)kz * Kc + 8 * g;
   const T* xp[MT];
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt) {
     int m = mb + mt * 16 + r;
     if (m >= a.M) m = a.M - 1;
-    xp[mt] = X + (int64_t)m * a.ldx + 8 * g;
+    const int xr = a.x_rows ? a.x_rows[m] : m;
+    xp[mt] = X + (int64_t)xr * a.ldx + (int64_t)kz * Kc + 8 * g;
   }
   float4_t acc[MT];
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt) acc[mt] = (float4_t){0.f, 0.f, 0.f, 0.f};
 
-  const int nsteps = a.K / 32;
-  int s = wave;
-  // unrolled by 4 steps to keep 4 weight loads in flight per lane
-  for (; s + 24 < nsteps; s += 32) {
-    Frag<T> wf[4];
+  const int nsteps = Kc / 32;
+  const int last = nsteps - 1;
+  for (int b0 = wave; b0 < nsteps; b0 += NW * U) {
+    Frag<T> wf[U];
+    Frag<T> xf[U][MT];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) frag_load(wf[u], wp + (s + 8 * u) * 32);
+    for (int u = 0; u < U; ++u) {
+      const int su = min(b0 + NW * u, last) * 32;
+      frag_load(wf[u], wp + su);
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-#pragma unroll
-      for (int mt = 0; mt < MT; ++mt) {
-        Frag<T> xf;
-        frag_load(xf, xp[mt] + (s + 8 * u) * 32);
-        mfma_step(acc[mt], wf[u], xf);
-      }
+      for (int mt = 0; mt < MT; ++mt) frag_load(xf[u][mt], xp[mt] + su);
     }
-  }
-  for (; s < nsteps; s += 8) {
-    Frag<T> wf;
-    frag_load(wf, wp + s * 32);
 #pragma unroll
-    for (int mt = 0; mt < MT; ++mt) {
-      Frag<T> xf;
-      frag_load(xf, xp[mt] + s * 32);
-      mfma_step(acc[mt], wf, xf);
+    for (int u = 0; u < U; ++u) {
+      if (b0 + NW * u < nsteps) {
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) mfma_step(acc[mt], wf[u], xf[u][mt]);
+      }
     }
   }
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt)
     *reinterpret_cast<float4_t*>(&red[wave][mt][lane][0]) = acc[mt];
   __syncthreads();
-  // 512 threads: thread -> (mt, lane) pairs; fixed-order sum over the 8 waves
+  // thread -> (mt, lane) pairs; fixed-order sum over the 8 waves
   for (int idx = tid; idx < MT * 64; idx += 512) {
     const int mt = idx >> 6, ln = idx & 63;
     float4_t v = *reinterpret_cast<float4_t*>(&red[0][mt][ln][0]);
 #pragma unroll
-    for (int w = 1; w < 8; ++w) v += *reinterpret_cast<float4_t*>(&red[w][mt][ln][0]);
+    for (int w = 1; w < NW; ++w) v += *reinterpret_cast<float4_t*>(&red[w][mt][ln][0]);
     const int m = mb + mt * 16 + (ln & 15);
     const int n = n0 + 4 * (ln >> 4);
     if (m >= a.M || n >= a.N) continue;
@@ -198,16 +201,140 @@ __global__ __launch_bounds__(512) void k_gemv_rows(GemmArgs a) {
         if (n + j < a.N) o[n + j] = v[j] + (a.bias ? a.bias[n + j] : 0.f);
       continue;
     }
+    if (EPI == EPI_PARTIAL) {
+      store4(a.out_f32 + ((int64_t)kz * a.M + m) * a.ldo + n, v[0], v[1], v[2], v[3]);
+      continue;
+    }
     if (a.bias) v += load4f(a.bias + n);
     epilogue_store<T, EPI>(a, m, 0, m, n, v);
   }
+}
+
+// ============================================================ tall-skinny GEMM, X through LDS
+// For 33..128 rows the X operand (L2-resident activations) costs more load bandwidth
+// than the weights when every 16-column tile re-reads it.  Here a 256-thread block
+// owns 64 columns (one 16-column tile per wave) and stages X[:, k-subchunk] in LDS
+// once for its 4 waves; each wave streams its weight rows (all loads of a subchunk in
+// flight before the first MFMA).  grid: (ceil(N/64), ceil(M/(16*MT)), ksplit).
+constexpr int XS_BYTES = 512;              // bytes of K per LDS subchunk row
+constexpr int XS_ROW = XS_BYTES + 16;      // padded row: conflict-free ds_read_b128
+template <typename T, int MT, int EPI>
+__global__ __launch_bounds__(256) void k_gemv_x(GemmArgs a) {
+  constexpr int KCH = XS_BYTES / (int)sizeof(T);  // k per subchunk (256 half / 128 float)
+  constexpr int KS = KCH / 32;                    // k-steps per subchunk
+  constexpr int CPR = XS_BYTES / 16;              // 16 B chunks per staged row (32)
+  constexpr int NCH = (MT * 16 * CPR) / 256;      // chunks per thread (= 2 MT)
+  __shared__ __attribute__((aligned(16))) char xs[MT * 16 * XS_ROW];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int r = lane & 15, g = lane >> 4;
+  const int n0 = blockIdx.x * 64 + wave * 16;
+  const int mb = blockIdx.y * (16 * MT);
+  const int kz = blockIdx.z;
+  const int Kc = a.K / gridDim.z;
+  const int kbase = kz * Kc;
+  const T* X = reinterpret_cast<const T*>(a.X);
+  const T* W = reinterpret_cast<const T*>(a.W);
+  int nrow = n0 + r;
+  if (nrow >= a.N) nrow = a.N - 1;
+  const T* wp = W + (int64_t)nrow * a.K + kbase + 8 * g;
+  // this thread's staging chunks: row = c / CPR, 16 B column ch = c % CPR
+  const char* xsrc[NCH];
+#pragma unroll
+  for (int i = 0; i < NCH; ++i) {
+    const int c = tid + 256 * i, row = c / CPR;
+    int m = mb + row;
+    if (m >= a.M) m = a.M - 1;
+    const int xr = a.x_rows ? a.x_rows[m] : m;
+    xsrc[i] = reinterpret_cast<const char*>(X + (int64_t)xr * a.ldx + kbase) + (c % CPR) * 16;
+  }
+  float4_t acc[MT];
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt) acc[mt] = (float4_t){0.f, 0.f, 0.f, 0.f};
+  Frag<T> wf[KS], wn[KS];
+  float4_t xr[NCH];
+  // issue the loads of subchunk kc (clamped addresses; ragged tails are masked later)
+  auto issue = [&](int kc, Frag<T>* w) {
+    const int ns = min(KCH, Kc - kc) / 32;
+    const int cpr = ns * 2 * (int)sizeof(T);  // valid 16 B chunks per row
+#pragma unroll
+    for (int s = 0; s < KS; ++s) frag_load(w[s], wp + kc + min(s, ns - 1) * 32);
+#pragma unroll
+    for (int i = 0; i < NCH; ++i) {
+      const int ch = (tid + 256 * i) % CPR;
+      xr[i] = *reinterpret_cast<const float4_t*>(xsrc[i] + (int64_t)kc * sizeof(T) + (min(ch, cpr - 1) - ch) * 16);
+    }
+  };
+  issue(0, wf);
+  for (int kc = 0; kc < Kc; kc += KCH) {
+    const int ns = min(KCH, Kc - kc) / 32;
+#pragma unroll
+    for (int i = 0; i < NCH; ++i) {
+      const int c = tid + 256 * i;
+      *reinterpret_cast<float4_t*>(xs + (c / CPR) * XS_ROW + (c % CPR) * 16) = xr[i];
+    }
+    __syncthreads();
+    const bool more = kc + KCH < Kc;
+    if (more) issue(kc + KCH, wn);  // next subchunk in flight during this one's MFMAs
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      if (s < ns) {
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) {
+          Frag<T> xf;
+          frag_load(xf, reinterpret_cast<const T*>(xs + (mt * 16 + r) * XS_ROW) + s * 32 + 8 * g);
+          mfma_step(acc[mt], wf[s], xf);
+        }
+      }
+    }
+    __syncthreads();
+    if (more) {
+#pragma unroll
+      for (int s = 0; s < KS; ++s) wf[s] = wn[s];
+    }
+  }
+  // lane holds Y[m = mb + mt*16 + r][n = n0 + 4g .. +3]
+  const int n = n0 + 4 * g;
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt) {
+    const int m = mb + mt * 16 + r;
+    if (m >= a.M || n >= a.N) continue;
+    float4_t v = acc[mt];
+    if (EPI == EPI_F32_COLS) {
+      float* o = a.out_f32 + (int64_t)m * a.ldo;
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if (n + j < a.N) o[n + j] = v[j] + (a.bias ? a.bias[n + j] : 0.f);
+      continue;
+    }
+    if (EPI == EPI_PARTIAL) {
+      store4(a.out_f32 + ((int64_t)kz * a.M + m) * a.ldo + n, v[0], v[1], v[2], v[3]);
+      continue;
+    }
+    if (a.bias) v += load4f(a.bias + n);
+    epilogue_store<T, EPI>(a, m, 0, m, n, v);
+  }
+}
+
+int gemv_ksplit(int M, int N, int K) {
+  // split-K for the residual projections: enough workgroups to cover the CUs,
+  // a divisor of the 32-wide step count, at most 16 slabs
+  const int mt = (M + 15) / 16;
+  const bool xpath = mt >= 3;  // k_gemv_x (EPI_PARTIAL with >= 33 rows)
+  const int rows_per = xpath ? (mt >= 8 ? 8 : mt) : (mt >= 8 ? 8 : mt);
+  const int wgs = (xpath ? (N + 63) / 64 : (N + 15) / 16) * ((M + 16 * rows_per - 1) / (16 * rows_per));
+  const int steps = K / 32;
+  int best = 1;
+  for (int z = 1; z <= 16; ++z)
+    if (steps % z == 0 && wgs * z <= 320) best = z;
+  return best;
 }
 
 // ============================================================ launchers
 template <typename T>
 int launch_gemm(const GemmArgs& a, int epi, hipStream_t st) {
   if (a.M <= 0) return 0;
-  const bool big = a.M > 128 && (a.N % TBN) == 0 && (a.K % (TKB / (int)sizeof(T))) == 0 && epi != EPI_F32_COLS;
+  const bool big = a.M > 128 && (a.N % TBN) == 0 && (a.K % (TKB / (int)sizeof(T))) == 0 && epi != EPI_F32_COLS &&
+                   epi != EPI_PARTIAL && a.x_rows == nullptr;
   if (big) {
     const int nwg = ((a.M + TBM - 1) / TBM) * (a.N / TBN);
     switch (epi) {
@@ -221,7 +348,32 @@ int launch_gemm(const GemmArgs& a, int epi, hipStream_t st) {
     if (a.x_group_rows != a.M && a.x_group_rows != 0 && a.x_group_rows < a.M) return -3;  // skinny: plain rows only
     const int mt = (a.M + 15) / 16;
     const int rows_per = mt >= 8 ? 8 : mt;
-    dim3 grid((a.N + 15) / 16, (a.M + 16 * rows_per - 1) / (16 * rows_per));
+    const int ks = epi == EPI_PARTIAL ? a.ksplit : 1;
+    if (ks < 1 || a.K % (32 * ks)) return -4;
+    if (mt >= 3 && (epi == EPI_PARTIAL || (a.N + 63) / 64 >= 70)) {  // tall-skinny: X shared via LDS by 4 column tiles
+      dim3 gx((a.N + 63) / 64, (a.M + 16 * rows_per - 1) / (16 * rows_per), ks);
+#define LAUNCHX(MT_)                                                                            \
+  switch (epi) {                                                                               \
+    case EPI_STORE: k_gemv_x<T, MT_, EPI_STORE><<<gx, 256, 0, st>>>(a); break;                  \
+    case EPI_STORE_GELU: k_gemv_x<T, MT_, EPI_STORE_GELU><<<gx, 256, 0, st>>>(a); break;        \
+    case EPI_RESID: k_gemv_x<T, MT_, EPI_RESID><<<gx, 256, 0, st>>>(a); break;                  \
+    case EPI_QKV_DEC: k_gemv_x<T, MT_, EPI_QKV_DEC><<<gx, 256, 0, st>>>(a); break;              \
+    case EPI_F32_COLS: k_gemv_x<T, MT_, EPI_F32_COLS><<<gx, 256, 0, st>>>(a); break;            \
+    case EPI_PARTIAL: k_gemv_x<T, MT_, EPI_PARTIAL><<<gx, 256, 0, st>>>(a); break;              \
+    default: return -1;                                                                        \
+  }
+      switch (rows_per) {
+        case 3: LAUNCHX(3) break;
+        case 4: LAUNCHX(4) break;
+        case 5: LAUNCHX(5) break;
+        case 6: LAUNCHX(6) break;
+        case 7: LAUNCHX(7) break;
+        default: LAUNCHX(8) break;
+      }
+#undef LAUNCHX
+      return 0;
+    }
+    dim3 grid((a.N + 15) / 16, (a.M + 16 * rows_per - 1) / (16 * rows_per), ks);
 #define LAUNCH(MT_)                                                                             \
   switch (epi) {                                                                               \
     case EPI_STORE: k_gemv_rows<T, MT_, EPI_STORE><<<grid, 512, 0, st>>>(a); break;             \
@@ -230,6 +382,7 @@ int launch_gemm(const GemmArgs& a, int epi, hipStream_t st) {
     case EPI_HEADSPLIT: k_gemv_rows<T, MT_, EPI_HEADSPLIT><<<grid, 512, 0, st>>>(a); break;     \
     case EPI_QKV_DEC: k_gemv_rows<T, MT_, EPI_QKV_DEC><<<grid, 512, 0, st>>>(a); break;         \
     case EPI_F32_COLS: k_gemv_rows<T, MT_, EPI_F32_COLS><<<grid, 512, 0, st>>>(a); break;       \
+    case EPI_PARTIAL: k_gemv_rows<T, MT_, EPI_PARTIAL><<<grid, 512, 0, st>>>(a); break;         \
     default: return -1;                                                                        \
   }
     switch (rows_per) {

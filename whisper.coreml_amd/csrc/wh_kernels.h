@@ -4,9 +4,14 @@
 
 namespace wh {
 
+constexpr int TKP = 1504;  // cross-KV keys per (window, head) block: 1500 padded to a multiple of 32
+
 template <typename T>
 void launch_layernorm(const float* x, T* y, const float* g, const float* b, int rows, int n, float eps,
                       const int* rows_in, hipStream_t st);
+template <typename T>
+void launch_resid_ln(float* x, const float* part, int nsplit, int64_t part_stride, const float* bias, T* y,
+                     const float* g, const float* b, int rows, int n, float eps, hipStream_t st);
 template <typename T>
 void launch_attn_enc(const T* qkv, int ld, int ns, int H, int Tlen, int nwin, int64_t wsi, T* out, int64_t wso,
                      hipStream_t st);

@@ -60,6 +60,85 @@ void launch_layernorm(const float* x, T* y, const float* g, const float* b, int 
   k_layernorm<T><<<(rows + 3) / 4, 256, 0, st>>>(x, y, g, b, rows, n, eps, rows_in);
 }
 
+// x[r] += bias + sum_s part[s][r] (fixed order: deterministic split-K reduction of the
+// residual GEMVs), then y = LayerNorm(x).  One 256-thread block per row; every load
+// of the row is issued before the first reduction (latency-bound at decode sizes).
+template <typename T, int NS>
+__global__ __launch_bounds__(256) void k_resid_ln(float* __restrict__ x, const float* __restrict__ part, int nsplit,
+                                                  int64_t part_stride, const float* __restrict__ bias,
+                                                  T* __restrict__ y, const float* __restrict__ gamma,
+                                                  const float* __restrict__ beta, int n, float eps) {
+  __shared__ float red[2][4];
+  const int row = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  float* xr = x + (int64_t)row * n;
+  constexpr int MAXV = 2;  // n <= 256 * 4 * 2 = 2048
+  const int nv = n >> 2;
+  float4_t v[MAXV];
+#pragma unroll
+  for (int i = 0; i < MAXV; ++i) {
+    const int c = tid + 256 * i;
+    if (c < nv) {
+      float4_t a = load4f(xr + 4 * c);
+      float4_t pp[NS > 0 ? NS : 1];
+#pragma unroll
+      for (int sp = 0; sp < NS; ++sp)
+        if (sp < nsplit) pp[sp] = load4f(part + sp * part_stride + (int64_t)row * n + 4 * c);
+      if (bias) a += load4f(bias + 4 * c);
+#pragma unroll
+      for (int sp = 0; sp < NS; ++sp)
+        if (sp < nsplit) a += pp[sp];
+      v[i] = a;
+    }
+  }
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < MAXV; ++i)
+    if (tid + 256 * i < nv) {
+      store4(xr + 4 * (tid + 256 * i), v[i][0], v[i][1], v[i][2], v[i][3]);
+      s += v[i][0] + v[i][1] + v[i][2] + v[i][3];
+    }
+  s = wave_sum(s);
+  if (lane == 0) red[0][wv] = s;
+  __syncthreads();
+  const float mean = (red[0][0] + red[0][1] + red[0][2] + red[0][3]) / (float)n;
+  float q = 0.f;
+#pragma unroll
+  for (int i = 0; i < MAXV; ++i)
+    if (tid + 256 * i < nv) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float d = v[i][j] - mean;
+        q += d * d;
+      }
+    }
+  q = wave_sum(q);
+  if (lane == 0) red[1][wv] = q;
+  __syncthreads();
+  const float rstd = rsqrtf((red[1][0] + red[1][1] + red[1][2] + red[1][3]) / (float)n + eps);
+  T* yr = y + (int64_t)row * n;
+#pragma unroll
+  for (int i = 0; i < MAXV; ++i) {
+    const int c = tid + 256 * i;
+    if (c < nv) {
+      const float4_t gm = load4f(gamma + 4 * c), bt = load4f(beta + 4 * c);
+      store4(yr + 4 * c, (v[i][0] - mean) * rstd * gm[0] + bt[0], (v[i][1] - mean) * rstd * gm[1] + bt[1],
+             (v[i][2] - mean) * rstd * gm[2] + bt[2], (v[i][3] - mean) * rstd * gm[3] + bt[3]);
+    }
+  }
+}
+
+template <typename T>
+void launch_resid_ln(float* x, const float* part, int nsplit, int64_t part_stride, const float* bias, T* y,
+                     const float* g, const float* b, int rows, int n, float eps, hipStream_t st) {
+  if (rows <= 0) return;
+  if (nsplit <= 0)
+    k_resid_ln<T, 0><<<rows, 256, 0, st>>>(x, part, 0, part_stride, bias, y, g, b, n, eps);
+  else if (nsplit <= 4)
+    k_resid_ln<T, 4><<<rows, 256, 0, st>>>(x, part, nsplit, part_stride, bias, y, g, b, n, eps);
+  else
+    k_resid_ln<T, 16><<<rows, 256, 0, st>>>(x, part, nsplit, part_stride, bias, y, g, b, n, eps);
+}
+
 // ============================================================ encoder flash attention (non-causal)
 // qkv: [T rows][ld] per window (q at col h*64, k at ns + h*64, v at 2ns + h*64); K is
 // pre-scaled by 1/8 (folded into Wk at load, exact).  out: [T][ns] per window.
@@ -203,9 +282,9 @@ __global__ __launch_bounds__(64) void k_self_attn(const T* __restrict__ q, int l
     }
   }
   const int64_t head_stride = (int64_t)ctx * 64;
-  auto kv_off = [&](int slot, int p) -> int64_t {
-    return ((((int64_t)w * nbeam + slot) * H + h) * head_stride) + (int64_t)p * 64;
-  };
+  const int64_t wbase = (int64_t)w * nbeam;
+  auto kv_off = [&](int slot, int p) -> int64_t { return ((wbase + slot) * H + h) * head_stride + (int64_t)p * 64; };
+  // scores: lane per key
   float mx = -INFINITY;
   for (int p = lane; p <= pos; p += 64) {
     const int slot = (p == pos) ? sl : an[p];
@@ -213,9 +292,11 @@ __global__ __launch_bounds__(64) void k_self_attn(const T* __restrict__ q, int l
     const T* kr = kc + kv_off(slot, p);
     float s = 0.f;
 #pragma unroll
-    for (int c = 0; c < 64; c += 4) {
-      const float4_t t = load4f(kr + c);
-      s += qv[c] * t[0] + qv[c + 1] * t[1] + qv[c + 2] * t[2] + qv[c + 3] * t[3];
+    for (int c = 0; c < 64; c += 8) {
+      Frag<T> f;
+      frag_load(f, kr + c);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) s += qv[c + e] * to_f32(f.v[e]);
     }
     sc[p] = s;
     mx = fmaxf(mx, s);
@@ -229,18 +310,42 @@ __global__ __launch_bounds__(64) void k_self_attn(const T* __restrict__ q, int l
   }
   sum = wave_sum(sum);
   __syncthreads();
-  // lane = output dim d
-  float o = 0.f;
-  int p = 0;
-  for (; p + 4 <= pos + 1; p += 4) {
-    const float v0 = to_f32(vc[kv_off(slot_of[p], p) + lane]);
-    const float v1 = to_f32(vc[kv_off(slot_of[p + 1], p + 1) + lane]);
-    const float v2 = to_f32(vc[kv_off(slot_of[p + 2], p + 2) + lane]);
-    const float v3 = to_f32(vc[kv_off(slot_of[p + 3], p + 3) + lane]);
-    o += sc[p] * v0 + sc[p + 1] * v1 + sc[p + 2] * v2 + sc[p + 3] * v3;
+  // P.V: lane = (key group kg = lane>>3, dim chunk dc = lane&7): 8 keys x 128 B per instruction
+  const int kg = lane >> 3, dc = (lane & 7) * 8;
+  float o[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) o[e] = 0.f;
+  int p = kg;
+  for (; p + 24 <= pos; p += 32) {  // 4 keys per lane in flight
+    Frag<T> f[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) frag_load(f[u], vc + kv_off(slot_of[p + 8 * u], p + 8 * u) + dc);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const float pw = sc[p + 8 * u];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o[e] += pw * to_f32(f[u].v[e]);
+    }
   }
-  for (; p <= pos; ++p) o += sc[p] * to_f32(vc[kv_off(slot_of[p], p) + lane]);
-  out[(int64_t)row * ldo + h * 64 + lane] = from_f32<T>(o / sum);
+  for (; p <= pos; p += 8) {
+    Frag<T> f;
+    frag_load(f, vc + kv_off(slot_of[p], p) + dc);
+    const float pw = sc[p];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] += pw * to_f32(f.v[e]);
+  }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    o[e] += __shfl_xor(o[e], 8, 64);
+    o[e] += __shfl_xor(o[e], 16, 64);
+    o[e] += __shfl_xor(o[e], 32, 64);
+  }
+  if (kg == 0) {
+    const float inv = 1.f / sum;
+    T* op = out + (int64_t)row * ldo + h * 64 + dc;
+    store4(op, o[0] * inv, o[1] * inv, o[2] * inv, o[3] * inv);
+    store4(op + 4, o[4] * inv, o[5] * inv, o[6] * inv, o[7] * inv);
+  }
 }
 
 template <typename T>
@@ -252,94 +357,140 @@ void launch_self_attn(const T* q, int ldq, const T* kc, const T* vc, const int* 
 }
 
 // ============================================================ decoder cross-attention (split-K flash decoding)
-// grid (windows, H, nsplit); block 256.  All rows of a window (beams, or prefill
-// tokens) share one pass over that split's keys: K/V are read from HBM once per
-// window per step.  ck/cv: [win][head][Tk][64] for this layer.
-// Partials: po[row][h][split][64], pm/pl[row][h][split].
+// grid (windows, H, nsplit), block 256 = 4 waves; wave w of split sp owns the 64-key
+// tile sp*4 + w.  All rows of a window (its beams, or the prefill tokens) share the
+// pass, in row tiles of 16: K and V of a window are streamed from HBM once per step.
+// Both MFMA operands load straight from HBM into fragments: K in its natural
+// [key][64] layout (A of S^T = K Q^T), V stored transposed [64][Tk] at encode time
+// (A of O^T = V^T P^T), so no LDS staging is needed; LDS only combines the 4 waves.
+// ck: [win][head][TKP][64], cvt: [win][head][64][TKP] (key-permuted) for this layer.
+// Partials per split: po[row][h][split][64], pm/pl[row][h][split] (k_cross_combine).
 // If qk_map != null the raw scores q.k of alignment heads are also written
-// (word timestamps, decoder.py:306-308): qk_out[(qk_map[h] * qk_rows + row) * Tk + key]
-// for heads with qk_map[h] >= 0.
-constexpr int XA_MAXR = 16;
+// (word timestamps, decoder.py:306-308): qk_out[(qk_map[h] * qk_rows + row) * Tk + key].
 template <typename T>
 __global__ __launch_bounds__(256) void k_cross_attn(const T* __restrict__ q, int ldq, const T* __restrict__ ck,
-                                                    const T* __restrict__ cv, int Tk, int H, int nsplit,
+                                                    const T* __restrict__ cvt, int Tk, int H, int nsplit,
                                                     const int* __restrict__ win_row0, const int* __restrict__ win_nrows,
                                                     const int* __restrict__ win_slot, int64_t win_stride,
                                                     float* __restrict__ po, float* __restrict__ pm, float* __restrict__ pl,
                                                     float* qk_out, const int* qk_map, int qk_rows) {
-  constexpr int CH = 192;  // max keys per split
-  __shared__ float qs[XA_MAXR][64];
-  __shared__ float sc[XA_MAXR][CH + 1];
-  __shared__ T vs[CH][64];
+  __shared__ float red_m[4][16], red_l[4][16];
+  __shared__ float red_o[4][64][17];
   const int wi = blockIdx.x, h = blockIdx.y, sp = blockIdx.z;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int r = lane & 15, g = lane >> 4;
   const int row0 = win_row0[wi], nrows = win_nrows[wi];
-  const int chunk = (Tk + nsplit - 1) / nsplit;
-  const int k0 = sp * chunk, k1 = min(Tk, k0 + chunk);
+  const int kt0 = (sp * 4 + wave) * 64;
+  const bool active = kt0 < Tk;
   const int qslot = qk_map ? qk_map[h] : -1;
-  const int nk = k1 - k0;
-  const T* kb = ck + (int64_t)win_slot[wi] * win_stride + (int64_t)h * Tk * 64;
-  const T* vb = cv + (int64_t)win_slot[wi] * win_stride + (int64_t)h * Tk * 64;
-  // stage V chunk
-  for (int c = tid; c < nk * 64 / 8; c += 256) {
-    const int key = c >> 3, part = c & 7;
-    const T* src = vb + (int64_t)(k0 + key) * 64 + part * 8;
+  const T* kbase = ck + (int64_t)win_slot[wi] * win_stride + (int64_t)h * TKP * 64;
+  const T* vbase = cvt + (int64_t)win_slot[wi] * win_stride + (int64_t)h * 64 * TKP;
+  constexpr float LOG2E = 1.4426950408889634f;
+  // K and V fragments of this wave's tile do not depend on the rows: load them once,
+  // all in flight together (V^T is key-permuted so each lane's 8 keys are contiguous)
+  Frag<T> kf[4][2], vf[4][2];
+  if (active) {
 #pragma unroll
-    for (int e = 0; e < 8; ++e) vs[key][part * 8 + e] = src[e];
-  }
-  // K row for this thread's key held in registers
-  float kr[64];
-  const bool has_key = tid < nk;
-  if (has_key) {
-    const T* src = kb + (int64_t)(k0 + tid) * 64;
-#pragma unroll
-    for (int c = 0; c < 64; c += 4) {
-      const float4_t t = load4f(src + c);
-      kr[c] = t[0]; kr[c + 1] = t[1]; kr[c + 2] = t[2]; kr[c + 3] = t[3];
+    for (int kt = 0; kt < 4; ++kt) {
+      const T* kp = kbase + (int64_t)(kt0 + kt * 16 + r) * 64 + 8 * g;
+      frag_load(kf[kt][0], kp);
+      frag_load(kf[kt][1], kp + 32);
     }
-  }
-  for (int rb = 0; rb < nrows; rb += XA_MAXR) {
-    const int nr = min(XA_MAXR, nrows - rb);
-    __syncthreads();
-    for (int c = tid; c < nr * 64; c += 256) {
-      const int i = c >> 6, d = c & 63;
-      qs[i][d] = to_f32(q[(int64_t)(row0 + rb + i) * ldq + h * 64 + d]);
-    }
-    __syncthreads();
-    if (has_key) {
-      for (int i = 0; i < nr; ++i) {
-        float s = 0.f;
 #pragma unroll
-        for (int d = 0; d < 64; ++d) s += qs[i][d] * kr[d];
-        sc[i][tid] = s;
-        if (qslot >= 0) qk_out[((int64_t)qslot * qk_rows + row0 + rb + i) * Tk + k0 + tid] = s;
+    for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+      for (int s = 0; s < 2; ++s) frag_load(vf[dt][s], vbase + (int64_t)(dt * 16 + r) * TKP + kt0 + 32 * s + 8 * g);
+  }
+  for (int rt = 0; rt < nrows; rt += 16) {
+    int qr = rt + r;
+    const bool qvalid = qr < nrows;
+    if (!qvalid) qr = nrows - 1;
+    float m = -INFINITY, l = 0.f;
+    float4_t acc[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) acc[i] = (float4_t){0.f, 0.f, 0.f, 0.f};
+    if (active) {
+      Frag<T> qf[2];
+      const T* qp = q + (int64_t)(row0 + qr) * ldq + h * 64 + 8 * g;
+      frag_load(qf[0], qp);
+      frag_load(qf[1], qp + 32);
+      float4_t sc[4];
+#pragma unroll
+      for (int kt = 0; kt < 4; ++kt) {
+        sc[kt] = (float4_t){0.f, 0.f, 0.f, 0.f};
+        mfma_step(sc[kt], kf[kt][0], qf[0]);
+        mfma_step(sc[kt], kf[kt][1], qf[1]);
       }
-    }
-    __syncthreads();
-    // per-row max / exp / sum: wave handles rows wave, wave+4, ...
-    for (int i = wave; i < nr; i += 4) {
       float mx = -INFINITY;
-      for (int k = lane; k < nk; k += 64) mx = fmaxf(mx, sc[i][k]);
-      mx = wave_max(mx);
-      float sm = 0.f;
-      for (int k = lane; k < nk; k += 64) {
-        const float e = __expf(sc[i][k] - mx);
-        sc[i][k] = e;
-        sm += e;
+#pragma unroll
+      for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int key = kt0 + kt * 16 + 4 * g + j;
+          if (key >= Tk) sc[kt][j] = -INFINITY;
+          else if (qslot >= 0 && qvalid) qk_out[((int64_t)qslot * qk_rows + row0 + qr) * Tk + key] = sc[kt][j];
+          mx = fmaxf(mx, sc[kt][j]);
+        }
+      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      m = mx;
+      Frag<T> pf[2];
+      float ps = 0.f;
+#pragma unroll
+      for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const float p = exp2f((sc[kt][j] - m) * LOG2E);
+          ps += p;
+          pf[kt >> 1].v[(kt & 1) * 4 + j] = from_f32<T>(p);
+        }
+      ps += __shfl_xor(ps, 16, 64);
+      ps += __shfl_xor(ps, 32, 64);
+      l = ps;
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt) mfma_step(acc[dt], vf[dt][s], pf[s]);
+    }
+    // combine the 4 waves of this split (lanes of every g hold the row stats of q = r)
+    if (g == 0) {
+      red_m[wave][r] = m;
+      red_l[wave][r] = l;
+    }
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) red_o[wave][dt * 16 + 4 * g + j][r] = acc[dt][j];
+    __syncthreads();
+    {
+      const int qq = tid >> 4, dc = (tid & 15) * 4;  // 16 rows x 16 chunks of 4 dims
+      float M = -INFINITY;
+#pragma unroll
+      for (int w = 0; w < 4; ++w) M = fmaxf(M, red_m[w][qq]);
+      float f[4], L = 0.f;
+#pragma unroll
+      for (int w = 0; w < 4; ++w) {
+        f[w] = red_m[w][qq] == -INFINITY ? 0.f : exp2f((red_m[w][qq] - M) * LOG2E);
+        L += f[w] * red_l[w][qq];
       }
-      sm = wave_sum(sm);
-      if (lane == 0) {
-        const int64_t pi = ((int64_t)(row0 + rb + i) * H + h) * nsplit + sp;
-        pm[pi] = mx;
-        pl[pi] = sm;
+      const int row = rt + qq;
+      if (row < nrows) {
+        const int64_t pi = ((int64_t)(row0 + row) * H + h) * nsplit + sp;
+        float o[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          o[e] = 0.f;
+#pragma unroll
+          for (int w = 0; w < 4; ++w) o[e] += f[w] * red_o[w][dc + e][qq];
+        }
+        store4(po + pi * 64 + dc, o[0], o[1], o[2], o[3]);
+        if (dc == 0) {
+          pm[pi] = M;
+          pl[pi] = L;
+        }
       }
     }
     __syncthreads();
-    for (int i = wave; i < nr; i += 4) {
-      float o = 0.f;
-      for (int k = 0; k < nk; ++k) o += sc[i][k] * to_f32(vs[k][lane]);
-      po[(((int64_t)(row0 + rb + i) * H + h) * nsplit + sp) * 64 + lane] = o;
-    }
   }
 }
 
@@ -366,6 +517,7 @@ void launch_cross_attn(const T* q, int ldq, const T* ck, const T* cv, int Tk, in
                        float* pm, float* pl, T* out, int ldo, int rows, float* qk_out, const int* qk_map, int qk_rows,
                        hipStream_t st) {
   if (rows <= 0) return;
+  nsplit = ((Tk + 63) / 64 + 3) / 4;  // one 64-key tile per wave, 4 waves per split
   k_cross_attn<T><<<dim3(nwin, H, nsplit), 256, 0, st>>>(q, ldq, ck, cv, Tk, H, nsplit, win_row0, win_nrows, win_slot,
                                                          win_stride, po, pm, pl, qk_out, qk_map, qk_rows);
   k_cross_combine<T><<<dim3(rows, H), 64, 0, st>>>(po, pm, pl, H, nsplit, out, ldo);
@@ -538,6 +690,8 @@ void launch_mel_norm(float* mel, int64_t count, int64_t ld, int n_mels, const un
 #define INST(T)                                                                                                     \
   template void launch_layernorm<T>(const float*, T*, const float*, const float*, int, int, float, const int*,     \
                                     hipStream_t);                                                                   \
+  template void launch_resid_ln<T>(float*, const float*, int, int64_t, const float*, T*, const float*, const float*, \
+                                   int, int, float, hipStream_t);                                                   \
   template void launch_attn_enc<T>(const T*, int, int, int, int, int, int64_t, T*, int64_t, hipStream_t);          \
   template void launch_self_attn<T>(const T*, int, const T*, const T*, const int*, const int*, const int*,         \
                                     const int*, int, int, int, int, T*, int, int, hipStream_t);                          \

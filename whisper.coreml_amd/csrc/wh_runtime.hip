@@ -49,6 +49,7 @@ constexpr int PRE_ROWS = 1024;    // prefill rows per pass
 constexpr int MROWS = 3008;       // melT rows per window (1 pad + 3000 + slack for padded conv1 K)
 constexpr int H1ROWS = 3002;      // conv1 output rows per window (zero rows 0 and 3001)
 constexpr int KC = 9;
+constexpr int RSPLIT = 16;      // max split-K slabs of the residual projections (decode rows <= 128)
 
 struct Arena {
   char* base = nullptr;
@@ -151,7 +152,7 @@ struct Ctx : public wh_ctx {
   std::vector<T*> kc, vc;
   // decoder buffers
   int RD;
-  float *x_d, *po, *pm, *pl, *logits, *logits2, *nsp;
+  float *x_d, *po, *pm, *pl, *logits, *logits2, *nsp, *part;
   T *xn_d, *q_d, *att_d, *hm_d;
   int *row_tok, *row_pos, *row_win, *row_slot, *win_row0, *win_nrows, *win_slot, *rows_in, *src_rows;
   int *st_row_win, *st_row_slot, *st_win_row0, *st_win_nrows, *st_win_slot;
@@ -255,12 +256,12 @@ struct Ctx : public wh_ctx {
     addA((size_t)WE * 1500 * n * 4); addA((size_t)WE * 1500 * n * sizeof(T)); addA((size_t)WE * 1500 * 3 * n * sizeof(T));
     addA((size_t)WE * 1500 * n * sizeof(T)); addA((size_t)WE * 1500 * 4 * n * sizeof(T));
     addA((size_t)Wcap * 1500 * n * sizeof(T));
-    addA((size_t)2 * Ld * Wcap * 1500 * n * sizeof(T));
+    addA((size_t)2 * Ld * Wcap * TKP * n * sizeof(T) + 65536);  // + slack: last key tile reads past TKP
     for (int l = 0; l < Ld; ++l) { addA((size_t)Wcap * Gcap * CTX * n * sizeof(T)); addA((size_t)Wcap * Gcap * CTX * n * sizeof(T)); }
     addA((size_t)RD * n * 4); addA((size_t)RD * n * sizeof(T)); addA((size_t)RD * n * sizeof(T)); addA((size_t)RD * n * sizeof(T));
     addA((size_t)RD * 4 * n * sizeof(T));
     addA((size_t)RD * nh * NSPLIT * 64 * 4); addA((size_t)RD * nh * NSPLIT * 4); addA((size_t)RD * nh * NSPLIT * 4);
-    addA((size_t)LR * V * 4); addA((size_t)2 * Wcap * V * 4); addA(Wcap * 4);
+    addA((size_t)LR * V * 4); addA((size_t)2 * Wcap * V * 4); addA(Wcap * 4); addA((size_t)RSPLIT * RD * n * 4);
     for (int i = 0; i < 9; ++i) addA(RD * 4);
     for (int i = 0; i < 5; ++i) addA(RD * 4);
     addA(Ld * nh * 4);
@@ -284,13 +285,13 @@ struct Ctx : public wh_ctx {
     x_e = fa((size_t)WE * 1500 * n); xn_e = ta((size_t)WE * 1500 * n); qkv_e = ta((size_t)WE * 1500 * 3 * n);
     att_e = ta((size_t)WE * 1500 * n); hm_e = ta((size_t)WE * 1500 * 4 * n);
     xa = ta((size_t)Wcap * 1500 * n);
-    ckv = ta((size_t)2 * Ld * Wcap * 1500 * n);
+    ckv = ta((size_t)2 * Ld * Wcap * TKP * n + 32768 / sizeof(T));
     kc.resize(Ld); vc.resize(Ld);
     for (int l = 0; l < Ld; ++l) { kc[l] = ta((size_t)Wcap * Gcap * CTX * n); vc[l] = ta((size_t)Wcap * Gcap * CTX * n); }
     x_d = fa((size_t)RD * n); xn_d = ta((size_t)RD * n); q_d = ta((size_t)RD * n); att_d = ta((size_t)RD * n);
     hm_d = ta((size_t)RD * 4 * n);
     po = fa((size_t)RD * nh * NSPLIT * 64); pm = fa((size_t)RD * nh * NSPLIT); pl = fa((size_t)RD * nh * NSPLIT);
-    logits = fa((size_t)LR * V); logits2 = fa((size_t)2 * Wcap * V); nsp = fa(Wcap);
+    logits = fa((size_t)LR * V); logits2 = fa((size_t)2 * Wcap * V); nsp = fa(Wcap); part = fa((size_t)RSPLIT * RD * n);
     row_tok = ia(RD); row_pos = ia(RD); row_win = ia(RD); row_slot = ia(RD); win_row0 = ia(RD); win_nrows = ia(RD);
     win_slot = ia(RD); rows_in = ia(RD); src_rows = ia(RD);
     st_row_win = ia(RD); st_row_slot = ia(RD); st_win_row0 = ia(RD); st_win_nrows = ia(RD); st_win_slot = ia(RD);
@@ -562,7 +563,7 @@ struct Ctx : public wh_ctx {
     // cross-KV for every decoder layer in one GEMM, written head-split [l2][slot][h][t][64]
     g = GemmArgs();
     g.x_group_rows = 1500; g.x_group_stride = (int64_t)1500 * n;
-    g.out = ckv; g.hs_state = n; g.hs_heads = nh; g.hs_T = 1500; g.hs_nslots = Wcap; g.hs_slot0 = s0;
+    g.out = ckv; g.hs_state = n; g.hs_heads = nh; g.hs_T = TKP; g.hs_nslots = Wcap; g.hs_slot0 = s0;
     TRY(gemm(xa_s, n, ckv_w, ckv_b, M, 2 * Ld * n, n, EPI_HEADSPLIT, g));
     return 0;
   }
@@ -598,13 +599,20 @@ struct Ctx : public wh_ctx {
   }
   int read_ckv(int slot, int layer, float* k, float* v) override {
     if (slot < 0 || slot >= Wcap || layer < 0 || layer >= Ld) return fail(-10, "slot/layer");
-    const size_t per = (size_t)nh * 1500 * 64;
+    const size_t per = (size_t)nh * TKP * 64;
     std::vector<T> h(per);
     for (int kv = 0; kv < 2; ++kv) {
       const T* src = ckv + ((size_t)(2 * layer + kv) * Wcap + slot) * per;
       HIPCHK(hipMemcpy(h.data(), src, per * sizeof(T), hipMemcpyDeviceToHost));
       float* o = kv ? v : k;
-      for (size_t i = 0; i < per; ++i) o[i] = (float)h[i];
+      for (int hh = 0; hh < nh; ++hh)
+        for (int t = 0; t < 1500; ++t) {
+          // K: [H][TKP][64]; V: transposed [H][64][TKP] with the 32-key permutation
+          const int q = t & 31, pt = (t & ~31) + 8 * ((q & 15) >> 2) + 4 * (q >> 4) + (q & 3);
+          for (int dd = 0; dd < 64; ++dd)
+            o[((size_t)hh * 1500 + t) * 64 + dd] =
+                kv ? (float)h[((size_t)hh * 64 + dd) * TKP + pt] : (float)h[((size_t)hh * TKP + t) * 64 + dd];
+        }
     }
     return 0;
   }
@@ -612,43 +620,61 @@ struct Ctx : public wh_ctx {
   // ------------------------------------------------------------ decoder layers
   // R rows of x_d (f32 residual); rw/rs/rp: row window / beam slot / position
   // ancG: beams per window in the anc table layout [w][ancG][ctx]; KV slots use Gcap
+  // residual projection x += X W^T + b, then xn = LayerNorm(x) with the NEXT norm's
+  // parameters.  Up to 128 rows: split-K weight streaming into fp32 partial slabs,
+  // summed in fixed order by k_resid_ln (deterministic, no atomics).  More rows:
+  // tile GEMM with an in-place residual epilogue.
+  int resid(const T* X, int K, const T* W, const float* b, int R, const float* lg, const float* lb) {
+    const int n = ns;
+    GemmArgs g;
+    if (R > 128) {
+      g.out_f32 = x_d; g.ldo = n;
+      TRY(gemm(X, K, W, b, R, n, K, EPI_RESID, g));
+      launch_resid_ln<T>(x_d, nullptr, 0, 0, nullptr, xn_d, lg, lb, R, n, 1e-5f, st);
+    } else {
+      const int ks = gemv_ksplit(R, n, K);
+      g.out_f32 = part; g.ldo = n; g.ksplit = ks;
+      TRY(gemm(X, K, W, nullptr, R, n, K, EPI_PARTIAL, g));
+      launch_resid_ln<T>(x_d, part, ks, (int64_t)R * n, b, xn_d, lg, lb, R, n, 1e-5f, st);
+    }
+    return 0;
+  }
+
+  // R rows of x_d (embeddings in, residual stream out); on exit xn_d holds the final
+  // decoder LayerNorm of every row (decoder.py:316).
   int dec_layers(int R, const int* rw, const int* rs, const int* rp, int ancG, int nwin, const int* wr0, const int* wnr,
                  const int* wsl, float* aqk, const int* qkmap, int qkrows) {
     const int n = ns;
     GemmArgs g;
+    launch_layernorm<T>(x_d, xn_d, dec[0].ln1_g, dec[0].ln1_b, R, n, 1e-5f, nullptr, st);
     for (int l = 0; l < Ld; ++l) {
       auto& e = dec[l];
-      launch_layernorm<T>(x_d, xn_d, e.ln1_g, e.ln1_b, R, n, 1e-5f, nullptr, st);
       g = GemmArgs();
       g.out = q_d; g.ldo = n; g.hs_state = n; g.hs_heads = nh;
       g.row_win = rw; g.row_slot = rs; g.row_pos = rp; g.kc = kc[l]; g.vc = vc[l]; g.kv_beams = Gcap; g.kv_ctx = CTX;
       TRY(gemm(xn_d, n, e.wqkv, e.bqkv, R, 3 * n, n, EPI_QKV_DEC, g));
       launch_self_attn<T>(q_d, n, kc[l], vc[l], rw, rs, rp, S.anc, ancG, Gcap, nh, CTX, att_d, n, R, st);
-      g = GemmArgs(); g.out_f32 = x_d; g.ldo = n;
-      TRY(gemm(att_d, n, e.wo, e.bo, R, n, n, EPI_RESID, g));
-      launch_layernorm<T>(x_d, xn_d, e.lnx_g, e.lnx_b, R, n, 1e-5f, nullptr, st);
+      TRY(resid(att_d, n, e.wo, e.bo, R, e.lnx_g, e.lnx_b));
       g = GemmArgs(); g.out = q_d; g.ldo = n;
       TRY(gemm(xn_d, n, e.wqx, e.bqx, R, n, n, EPI_STORE, g));
-      const T* ck = ckv + (size_t)(2 * l) * Wcap * 1500 * n;
-      const T* cv = ckv + (size_t)(2 * l + 1) * Wcap * 1500 * n;
-      launch_cross_attn<T>(q_d, n, ck, cv, 1500, nh, NSPLIT, nwin, wr0, wnr, wsl, (int64_t)1500 * n, po, pm, pl, att_d,
+      const T* ck = ckv + (size_t)(2 * l) * Wcap * TKP * n;
+      const T* cv = ckv + (size_t)(2 * l + 1) * Wcap * TKP * n;
+      launch_cross_attn<T>(q_d, n, ck, cv, 1500, nh, NSPLIT, nwin, wr0, wnr, wsl, (int64_t)TKP * n, po, pm, pl, att_d,
                            n, R, aqk, qkmap ? qkmap + l * nh : nullptr, qkrows, st);
-      g = GemmArgs(); g.out_f32 = x_d; g.ldo = n;
-      TRY(gemm(att_d, n, e.wox, e.box, R, n, n, EPI_RESID, g));
-      launch_layernorm<T>(x_d, xn_d, e.ln2_g, e.ln2_b, R, n, 1e-5f, nullptr, st);
+      TRY(resid(att_d, n, e.wox, e.box, R, e.ln2_g, e.ln2_b));
       g = GemmArgs(); g.out = hm_d; g.ldo = 4 * n;
       TRY(gemm(xn_d, n, e.w1, e.b1, R, 4 * n, n, EPI_STORE_GELU, g));
-      g = GemmArgs(); g.out_f32 = x_d; g.ldo = n;
-      TRY(gemm(hm_d, 4 * n, e.w2, e.b2, R, n, 4 * n, EPI_RESID, g));
+      const bool last = l + 1 == Ld;
+      TRY(resid(hm_d, 4 * n, e.w2, e.b2, R, last ? ln_g : dec[l + 1].ln1_g, last ? ln_b : dec[l + 1].ln1_b));
     }
     return 0;
   }
 
-  int vocab(const float* xrows_src, const int* rows_sel, int R, float* out) {
-    // final LayerNorm (eps 1e-5) on selected rows, then logits = x E^T (decoder.py:238-240, 316-320)
-    launch_layernorm<T>(xrows_src, xn_d, ln_g, ln_b, R, ns, 1e-5f, rows_sel, st);
+  // logits = LN(x) E^T for R rows of xn_d (optionally gathered by rows_sel)
+  // (decoder.py:238-240, 316-320)
+  int vocab(const int* rows_sel, int R, float* out) {
     GemmArgs g;
-    g.out_f32 = out; g.ldo = V;
+    g.out_f32 = out; g.ldo = V; g.x_rows = rows_sel;
     return gemm(xn_d, ns, E, nullptr, R, V, ns, EPI_F32_COLS, g);
   }
 
@@ -705,7 +731,7 @@ struct Ctx : public wh_ctx {
     HIPCHK(hipMemcpyAsync(rows_in, sel.data(), sel.size() * 4, hipMemcpyHostToDevice, st));
     launch_embed<T>(E, Pdec, ns, row_tok, row_pos, nullptr, nullptr, 1, HCTX, CTX - 1, x_d, R, st);
     TRY(dec_layers(R, row_win, row_slot, row_pos, S.G, nw, win_row0, win_nrows, win_slot, nullptr, nullptr, 0));
-    TRY(vocab(x_d, rows_in, 2 * nw, logits2 + (size_t)2 * w0 * V));
+    TRY(vocab(rows_in, 2 * nw, logits2 + (size_t)2 * w0 * V));
     (void)first_update_rows;
     // the host vectors must outlive the async copies
     HIPCHK(hipStreamSynchronize(st));
@@ -801,7 +827,7 @@ struct Ctx : public wh_ctx {
     launch_embed<T>(E, Pdec, ns, nullptr, row_pos, S.hist, S.len, cur_G, HCTX, CTX - 1, x_d, R, st);
     TRY(dec_layers(R, st_row_win, st_row_slot, row_pos, cur_G, cur_nwin, st_win_row0, st_win_nrows, st_win_slot,
                    nullptr, nullptr, 0));
-    TRY(vocab(x_d, nullptr, R, logits));
+    TRY(vocab(nullptr, R, logits));
     launch_logit_rows(logits, V, S, O, cur_nwin, st);
     launch_merge(S, O, cur_nwin, st);
     return 0;
@@ -828,15 +854,28 @@ struct Ctx : public wh_ctx {
     return 0;
   }
 
+  // WHISPER_HIP_EAGER=1 launches the step kernels directly instead of replaying the
+  // captured graph (same kernels; used under profilers that do not follow graphs)
+  bool eager() const {
+    const char* e = getenv("WHISPER_HIP_EAGER");
+    return e && e[0] == '1';
+  }
+
+  int launch_step() {
+    if (eager()) return step_body();
+    HIPCHK(hipGraphLaunch(gexec, st));
+    return 0;
+  }
+
   int decode_steps(int max_steps, int* n_done) override {
     if (cur_nwin < 1) return fail(-13, "no decode in progress");
-    TRY(ensure_graph());
+    if (!eager()) TRY(ensure_graph());
     hipEventRecord(tm.a, st);
     int steps = 0, done = 0;
     const int chunk = 8;
     while (steps < max_steps) {
       const int k = std::min(chunk, max_steps - steps);
-      for (int i = 0; i < k; ++i) HIPCHK(hipGraphLaunch(gexec, st));
+      for (int i = 0; i < k; ++i) TRY(launch_step());
       steps += k;
       HIPCHK(hipMemcpyAsync(h_done, S.done, cur_nwin * 4, hipMemcpyDeviceToHost, st));
       HIPCHK(hipStreamSynchronize(st));
@@ -906,7 +945,7 @@ struct Ctx : public wh_ctx {
     for (int r0 = 0; r0 < n && rc == 0; r0 += 128) {
       const int rr = std::min(128, n - r0);
       if (hipMemcpyAsync(rows_in, s2.data() + r0, rr * 4, hipMemcpyHostToDevice, st) != hipSuccess) rc = -100;
-      if (!rc) rc = vocab(x_d, rows_in, rr, out + (size_t)r0 * V);
+      if (!rc) rc = vocab(rows_in, rr, out + (size_t)r0 * V);
       if (!rc && hipStreamSynchronize(st) != hipSuccess) rc = -100;
     }
     if (!rc && hipMemcpyAsync(lg, out, (size_t)n * V * 4, hipMemcpyDeviceToHost, st) != hipSuccess) rc = -100;
@@ -924,9 +963,9 @@ struct Ctx : public wh_ctx {
   int time_stage(int what, int iters, double* ms) override {
     if (what == 0) {
       if (cur_nwin < 1) return fail(-16, "no decode batch");
-      TRY(ensure_graph());
+      if (!eager()) TRY(ensure_graph());
       hipEventRecord(tm.a, st);
-      for (int i = 0; i < iters; ++i) HIPCHK(hipGraphLaunch(gexec, st));
+      for (int i = 0; i < iters; ++i) TRY(launch_step());
       hipEventRecord(tm.b, st);
     } else {
       hipEventRecord(tm.a, st);
