@@ -95,7 +95,7 @@ WH_DEV void epilogue_store(const GemmArgs& a, int m, int gi, int ri, int n, floa
 template <typename T>
 int launch_gemm(const GemmArgs& a, int epi, hipStream_t st);
 
-// split-K factor the skinny paths use for EPI_PARTIAL at this shape (<= 16)
-int gemv_ksplit(int M, int N, int K);
+// split-K factor the skinny paths use for EPI_PARTIAL at this shape (<= min(16, max_z))
+int gemv_ksplit(int M, int N, int K, int max_z = 16);
 
 }  // namespace wh

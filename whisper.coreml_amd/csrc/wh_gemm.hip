@@ -315,7 +315,7 @@ __global__ __launch_bounds__(256) void k_gemv_x(GemmArgs a) {
   }
 }
 
-int gemv_ksplit(int M, int N, int K) {
+int gemv_ksplit(int M, int N, int K, int max_z) {
   // split-K for the residual projections: enough workgroups to cover the CUs,
   // a divisor of the 32-wide step count, at most 16 slabs
   const int mt = (M + 15) / 16;
@@ -324,7 +324,7 @@ int gemv_ksplit(int M, int N, int K) {
   const int wgs = (xpath ? (N + 63) / 64 : (N + 15) / 16) * ((M + 16 * rows_per - 1) / (16 * rows_per));
   const int steps = K / 32;
   int best = 1;
-  for (int z = 1; z <= 16; ++z)
+  for (int z = 1; z <= 16 && z <= max_z; ++z)
     if (steps % z == 0 && wgs * z <= 320) best = z;
   return best;
 }

@@ -20,6 +20,13 @@ void launch_self_attn(const T* q, int ldq, const T* kc, const T* vc, const int* 
                       const int* anc, int anc_beams, int nbeam, int H, int ctx, T* out, int ldo, int rows,
                       hipStream_t st);
 template <typename T>
+void launch_self_attn_qkv(const float* part, int nsplit, int64_t part_stride, const float* bqkv, int ns, T* kc, T* vc,
+                          const int* rw, const int* rs, const int* rp, const int* anc, int anc_beams, int nbeam, int H,
+                          int ctx, T* out, int ldo, int rows, hipStream_t st);
+template <typename T>
+void launch_reduce_store(const float* part, int nsplit, int64_t part_stride, const float* bias, T* out, int ldo, int M,
+                         int N, int gelu, hipStream_t st);
+template <typename T>
 void launch_cross_attn(const T* q, int ldq, const T* ck, const T* cv, int Tk, int H, int nsplit, int nwin,
                        const int* win_row0, const int* win_nrows, const int* win_slot, int64_t win_stride, float* po,
                        float* pm, float* pl, T* out, int ldo, int rows, float* qk_out, const int* qk_map, int qk_rows,

@@ -356,6 +356,169 @@ void launch_self_attn(const T* q, int ldq, const T* kc, const T* vc, const int* 
   k_self_attn<T><<<dim3(rows, H), 64, 0, st>>>(q, ldq, kc, vc, rw, rs, rp, anc, anc_beams, nbeam, H, ctx, out, ldo);
 }
 
+// Step-mode variant: the QKV projection arrives as split-K fp32 partial slabs
+// part[z][row][3n] (k_gemv_*, EPI_PARTIAL).  Each (row, head) wave sums its q/k/v
+// slices in fixed order, adds the bias, writes k/v (rounded to T) into its own slot
+// at position pos and attends with them directly (no read-back of the fresh row).
+// Only valid when no other row of the launch needs this row's K/V (one row per beam).
+template <typename T>
+__global__ __launch_bounds__(64) void k_self_attn_qkv(const float* __restrict__ part, int nsplit, int64_t part_stride,
+                                                      const float* __restrict__ bqkv, int ns, T* __restrict__ kc,
+                                                      T* __restrict__ vc, const int* __restrict__ row_win,
+                                                      const int* __restrict__ row_slot, const int* __restrict__ row_pos,
+                                                      const int* __restrict__ anc, int anc_beams, int nbeam, int H,
+                                                      int ctx, T* __restrict__ out, int ldo) {
+  __shared__ float sc[512];
+  __shared__ int slot_of[512];
+  __shared__ float qs[64], vs[64];
+  const int row = blockIdx.x, h = blockIdx.y, lane = threadIdx.x;
+  const int w = row_win[row], sl = row_slot[row], pos = row_pos[row];
+  const int* an = anc + ((int64_t)w * anc_beams + sl) * ctx;
+  const int64_t head_stride = (int64_t)ctx * 64;
+  const int64_t wbase = (int64_t)w * nbeam;
+  auto kv_off = [&](int slot, int p) -> int64_t { return ((wbase + slot) * H + h) * head_stride + (int64_t)p * 64; };
+  // q/k/v of this row and head: lane = d
+  float qd, kd, vd;
+  {
+    const float* pr = part + (int64_t)row * 3 * ns + h * 64 + lane;
+    float a0[16], a1[16], a2[16];
+#pragma unroll
+    for (int z = 0; z < 16; ++z)
+      if (z < nsplit) {
+        a0[z] = pr[z * part_stride];
+        a1[z] = pr[z * part_stride + ns];
+        a2[z] = pr[z * part_stride + 2 * ns];
+      }
+    qd = bqkv[h * 64 + lane];
+    kd = bqkv[ns + h * 64 + lane];
+    vd = bqkv[2 * ns + h * 64 + lane];
+#pragma unroll
+    for (int z = 0; z < 16; ++z)
+      if (z < nsplit) {
+        qd += a0[z];
+        kd += a1[z];
+        vd += a2[z];
+      }
+  }
+  const T qT = from_f32<T>(qd), kT = from_f32<T>(kd), vT = from_f32<T>(vd);
+  kc[kv_off(sl, pos) + lane] = kT;
+  vc[kv_off(sl, pos) + lane] = vT;
+  qs[lane] = to_f32(qT);
+  vs[lane] = to_f32(vT);
+  const float s_cur = wave_sum(to_f32(qT) * to_f32(kT));
+  __syncthreads();
+  float qv[64];
+#pragma unroll
+  for (int c = 0; c < 64; ++c) qv[c] = qs[c];
+  // scores of the cached positions p < pos: lane per key
+  float mx = s_cur;
+  for (int p = lane; p < pos; p += 64) {
+    const int slot = an[p];
+    slot_of[p] = slot;
+    const T* kr = kc + kv_off(slot, p);
+    float s = 0.f;
+#pragma unroll
+    for (int c = 0; c < 64; c += 8) {
+      Frag<T> f;
+      frag_load(f, kr + c);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) s += qv[c + e] * to_f32(f.v[e]);
+    }
+    sc[p] = s;
+    mx = fmaxf(mx, s);
+  }
+  mx = wave_max(mx);
+  float sum = 0.f;
+  for (int p = lane; p < pos; p += 64) {
+    const float e = __expf(sc[p] - mx);
+    sc[p] = e;
+    sum += e;
+  }
+  const float e_cur = __expf(s_cur - mx);
+  sum = wave_sum(sum) + e_cur;
+  __syncthreads();
+  const int kg = lane >> 3, dc = (lane & 7) * 8;
+  float o[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) o[e] = 0.f;
+  int p = kg;
+  for (; p + 24 < pos; p += 32) {
+    Frag<T> f[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) frag_load(f[u], vc + kv_off(slot_of[p + 8 * u], p + 8 * u) + dc);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const float pw = sc[p + 8 * u];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o[e] += pw * to_f32(f[u].v[e]);
+    }
+  }
+  for (; p < pos; p += 8) {
+    Frag<T> f;
+    frag_load(f, vc + kv_off(slot_of[p], p) + dc);
+    const float pw = sc[p];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] += pw * to_f32(f.v[e]);
+  }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    o[e] += __shfl_xor(o[e], 8, 64);
+    o[e] += __shfl_xor(o[e], 16, 64);
+    o[e] += __shfl_xor(o[e], 32, 64);
+  }
+  if (kg == 0) {
+    const float inv = 1.f / sum;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] = (o[e] + e_cur * vs[dc + e]) * inv;
+    T* op = out + (int64_t)row * ldo + h * 64 + dc;
+    store4(op, o[0], o[1], o[2], o[3]);
+    store4(op + 4, o[4], o[5], o[6], o[7]);
+  }
+}
+
+template <typename T>
+void launch_self_attn_qkv(const float* part, int nsplit, int64_t part_stride, const float* bqkv, int ns, T* kc, T* vc,
+                          const int* rw, const int* rs, const int* rp, const int* anc, int anc_beams, int nbeam, int H,
+                          int ctx, T* out, int ldo, int rows, hipStream_t st) {
+  if (rows <= 0) return;
+  k_self_attn_qkv<T><<<dim3(rows, H), 64, 0, st>>>(part, nsplit, part_stride, bqkv, ns, kc, vc, rw, rs, rp, anc,
+                                                   anc_beams, nbeam, H, ctx, out, ldo);
+}
+
+// out[m][n] = act(bias[n] + sum_z part[z][m][n]) as T (split-K epilogue of the
+// non-residual decoder GEMVs: cross-attention query, MLP fc1 + GELU)
+template <typename T, int ACT>
+__global__ __launch_bounds__(256) void k_reduce_store(const float* __restrict__ part, int nsplit, int64_t part_stride,
+                                                      const float* __restrict__ bias, T* __restrict__ out, int ldo, int M,
+                                                      int N) {
+  const int64_t i = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4;
+  if (i >= (int64_t)M * N) return;
+  const int m = (int)(i / N), n = (int)(i - (int64_t)m * N);
+  float4_t pp[16];
+#pragma unroll
+  for (int z = 0; z < 16; ++z)
+    if (z < nsplit) pp[z] = load4f(part + z * part_stride + i);
+  float4_t v = bias ? load4f(bias + n) : (float4_t){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int z = 0; z < 16; ++z)
+    if (z < nsplit) v += pp[z];
+  if (ACT) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[j] = gelu_f(v[j]);
+  }
+  store4(out + (int64_t)m * ldo + n, v[0], v[1], v[2], v[3]);
+}
+
+template <typename T>
+void launch_reduce_store(const float* part, int nsplit, int64_t part_stride, const float* bias, T* out, int ldo, int M,
+                         int N, int gelu, hipStream_t st) {
+  if (M <= 0) return;
+  const int64_t tot = (int64_t)M * N / 4;
+  const unsigned nb = (unsigned)((tot + 255) / 256);
+  if (gelu) k_reduce_store<T, 1><<<nb, 256, 0, st>>>(part, nsplit, part_stride, bias, out, ldo, M, N);
+  else k_reduce_store<T, 0><<<nb, 256, 0, st>>>(part, nsplit, part_stride, bias, out, ldo, M, N);
+}
+
 // ============================================================ decoder cross-attention (split-K flash decoding)
 // grid (windows, H, nsplit), block 256 = 4 waves; wave w of split sp owns the 64-key
 // tile sp*4 + w.  All rows of a window (its beams, or the prefill tokens) share the
@@ -692,6 +855,9 @@ void launch_mel_norm(float* mel, int64_t count, int64_t ld, int n_mels, const un
                                     hipStream_t);                                                                   \
   template void launch_resid_ln<T>(float*, const float*, int, int64_t, const float*, T*, const float*, const float*, \
                                    int, int, float, hipStream_t);                                                   \
+  template void launch_self_attn_qkv<T>(const float*, int, int64_t, const float*, int, T*, T*, const int*, const int*, \
+                                        const int*, const int*, int, int, int, int, T*, int, int, hipStream_t);     \
+  template void launch_reduce_store<T>(const float*, int, int64_t, const float*, T*, int, int, int, int, hipStream_t); \
   template void launch_attn_enc<T>(const T*, int, int, int, int, int, int64_t, T*, int64_t, hipStream_t);          \
   template void launch_self_attn<T>(const T*, int, const T*, const T*, const int*, const int*, const int*,         \
                                     const int*, int, int, int, int, T*, int, int, hipStream_t);                          \

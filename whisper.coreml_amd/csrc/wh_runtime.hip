@@ -624,6 +624,9 @@ struct Ctx : public wh_ctx {
   // parameters.  Up to 128 rows: split-K weight streaming into fp32 partial slabs,
   // summed in fixed order by k_resid_ln (deterministic, no atomics).  More rows:
   // tile GEMM with an in-place residual epilogue.
+  // how many [R][N] fp32 slabs fit in the partial buffer
+  int part_slabs(int R, int N) const { return (int)std::min<int64_t>(16, (int64_t)RSPLIT * RD * ns / ((int64_t)R * N)); }
+
   int resid(const T* X, int K, const T* W, const float* b, int R, const float* lg, const float* lb) {
     const int n = ns;
     GemmArgs g;
@@ -632,7 +635,7 @@ struct Ctx : public wh_ctx {
       TRY(gemm(X, K, W, b, R, n, K, EPI_RESID, g));
       launch_resid_ln<T>(x_d, nullptr, 0, 0, nullptr, xn_d, lg, lb, R, n, 1e-5f, st);
     } else {
-      const int ks = gemv_ksplit(R, n, K);
+      const int ks = gemv_ksplit(R, n, K, part_slabs(R, n));
       g.out_f32 = part; g.ldo = n; g.ksplit = ks;
       TRY(gemm(X, K, W, nullptr, R, n, K, EPI_PARTIAL, g));
       launch_resid_ln<T>(x_d, part, ks, (int64_t)R * n, b, xn_d, lg, lb, R, n, 1e-5f, st);
@@ -640,30 +643,55 @@ struct Ctx : public wh_ctx {
     return 0;
   }
 
+  // out = act(xn W^T + b) for R rows (cross-attention query, MLP fc1): split-K
+  // partial slabs + fixed-order reduce in step mode, the direct GEMM otherwise
+  int proj(const T* W, const float* b, int R, int N, T* out, int gelu, bool skinny) {
+    GemmArgs g;
+    if (skinny) {
+      const int ks = gemv_ksplit(R, N, ns, part_slabs(R, N));
+      g.out_f32 = part; g.ldo = N; g.ksplit = ks;
+      TRY(gemm(xn_d, ns, W, nullptr, R, N, ns, EPI_PARTIAL, g));
+      launch_reduce_store<T>(part, ks, (int64_t)R * N, b, out, N, R, N, gelu, st);
+    } else {
+      g.out = out; g.ldo = N;
+      TRY(gemm(xn_d, ns, W, b, R, N, ns, gelu ? EPI_STORE_GELU : EPI_STORE, g));
+    }
+    return 0;
+  }
+
   // R rows of x_d (embeddings in, residual stream out); on exit xn_d holds the final
   // decoder LayerNorm of every row (decoder.py:316).
   int dec_layers(int R, const int* rw, const int* rs, const int* rp, int ancG, int nwin, const int* wr0, const int* wnr,
-                 const int* wsl, float* aqk, const int* qkmap, int qkrows) {
+                 const int* wsl, float* aqk, const int* qkmap, int qkrows, bool step = false) {
     const int n = ns;
+    // step mode (one row per beam, rows independent): the skinny projections run
+    // split-K into fp32 partial slabs; QKV's reduction is fused into self-attention
+    const bool skinny = step && R <= 128;
     GemmArgs g;
     launch_layernorm<T>(x_d, xn_d, dec[0].ln1_g, dec[0].ln1_b, R, n, 1e-5f, nullptr, st);
     for (int l = 0; l < Ld; ++l) {
       auto& e = dec[l];
-      g = GemmArgs();
-      g.out = q_d; g.ldo = n; g.hs_state = n; g.hs_heads = nh;
-      g.row_win = rw; g.row_slot = rs; g.row_pos = rp; g.kc = kc[l]; g.vc = vc[l]; g.kv_beams = Gcap; g.kv_ctx = CTX;
-      TRY(gemm(xn_d, n, e.wqkv, e.bqkv, R, 3 * n, n, EPI_QKV_DEC, g));
-      launch_self_attn<T>(q_d, n, kc[l], vc[l], rw, rs, rp, S.anc, ancG, Gcap, nh, CTX, att_d, n, R, st);
+      if (skinny) {
+        const int ks = gemv_ksplit(R, 3 * n, n, part_slabs(R, 3 * n));
+        g = GemmArgs(); g.out_f32 = part; g.ldo = 3 * n; g.ksplit = ks;
+        TRY(gemm(xn_d, n, e.wqkv, nullptr, R, 3 * n, n, EPI_PARTIAL, g));
+        launch_self_attn_qkv<T>(part, ks, (int64_t)R * 3 * n, e.bqkv, n, kc[l], vc[l], rw, rs, rp, S.anc, ancG, Gcap,
+                                nh, CTX, att_d, n, R, st);
+      } else {
+        g = GemmArgs();
+        g.out = q_d; g.ldo = n; g.hs_state = n; g.hs_heads = nh;
+        g.row_win = rw; g.row_slot = rs; g.row_pos = rp; g.kc = kc[l]; g.vc = vc[l]; g.kv_beams = Gcap; g.kv_ctx = CTX;
+        TRY(gemm(xn_d, n, e.wqkv, e.bqkv, R, 3 * n, n, EPI_QKV_DEC, g));
+        launch_self_attn<T>(q_d, n, kc[l], vc[l], rw, rs, rp, S.anc, ancG, Gcap, nh, CTX, att_d, n, R, st);
+      }
       TRY(resid(att_d, n, e.wo, e.bo, R, e.lnx_g, e.lnx_b));
-      g = GemmArgs(); g.out = q_d; g.ldo = n;
-      TRY(gemm(xn_d, n, e.wqx, e.bqx, R, n, n, EPI_STORE, g));
+      TRY(proj(e.wqx, e.bqx, R, n, q_d, 0, skinny));
       const T* ck = ckv + (size_t)(2 * l) * Wcap * TKP * n;
       const T* cv = ckv + (size_t)(2 * l + 1) * Wcap * TKP * n;
       launch_cross_attn<T>(q_d, n, ck, cv, 1500, nh, NSPLIT, nwin, wr0, wnr, wsl, (int64_t)TKP * n, po, pm, pl, att_d,
                            n, R, aqk, qkmap ? qkmap + l * nh : nullptr, qkrows, st);
       TRY(resid(att_d, n, e.wox, e.box, R, e.ln2_g, e.ln2_b));
-      g = GemmArgs(); g.out = hm_d; g.ldo = 4 * n;
-      TRY(gemm(xn_d, n, e.w1, e.b1, R, 4 * n, n, EPI_STORE_GELU, g));
+      TRY(proj(e.w1, e.b1, R, 4 * n, hm_d, 1, skinny));
       const bool last = l + 1 == Ld;
       TRY(resid(hm_d, 4 * n, e.w2, e.b2, R, last ? ln_g : dec[l + 1].ln1_g, last ? ln_b : dec[l + 1].ln1_b));
     }
@@ -826,7 +854,7 @@ struct Ctx : public wh_ctx {
     const int R = cur_nwin * cur_G;
     launch_embed<T>(E, Pdec, ns, nullptr, row_pos, S.hist, S.len, cur_G, HCTX, CTX - 1, x_d, R, st);
     TRY(dec_layers(R, st_row_win, st_row_slot, row_pos, cur_G, cur_nwin, st_win_row0, st_win_nrows, st_win_slot,
-                   nullptr, nullptr, 0));
+                   nullptr, nullptr, 0, true));
     TRY(vocab(nullptr, R, logits));
     launch_logit_rows(logits, V, S, O, cur_nwin, st);
     launch_merge(S, O, cur_nwin, st);
