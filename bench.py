@@ -84,6 +84,34 @@ def decoder_step_bytes(dims, n_windows, beams, mean_ctx, elem=2):
     return weights + cross + selfkv
 
 
+def projection_bytes_per_launch(dims, rows, elem=2):
+    """Algorithmic bytes of one split-K projection GEMV, averaged over the six per
+    decoder layer (qkv n->3n, out n->n, cross-q n->n, cross-out n->n, fc1 n->4n,
+    fc2 4n->n): weights N*K + activations rows*K (fp16) + fp32 result rows*N."""
+    n = dims["n_text_state"]
+    shapes = [(3 * n, n), (n, n), (n, n), (n, n), (4 * n, n), (n, 4 * n)]
+    tot = sum(N * K * elem + rows * K * elem + rows * N * 4 for N, K in shapes)
+    return tot // len(shapes)
+
+
+def cross_attn_bytes_per_launch(dims, n_windows, rows, elem=2):
+    """One layer's cross-attention: K and V of every window (2*1500*n) + q in / out."""
+    n = dims["n_text_state"]
+    return n_windows * 2 * 1500 * n * elem + 2 * rows * n * elem
+
+
+def load_traffic(kernel):
+    """HBM bytes per launch of `kernel` from the committed PMC pass
+    (profiles/<round>/traffic.json, written by profiles/pmc_traffic.py: FETCH_SIZE x2
+    + WRITE_SIZE per the gfx950 correction of MI355X_MICROARCH.md), or None."""
+    path = os.path.join(REPO, "profiles", "r01", "traffic.json")
+    try:
+        with open(path) as f:
+            return json.load(f)[kernel]["hbm_bytes_per_launch"]
+    except (OSError, KeyError, ValueError):
+        return None
+
+
 def encoder_flops(dims):
     n, L, T = dims["n_audio_state"], dims["n_audio_layer"], 1500
     conv = 2 * 3000 * dims["n_mels"] * 3 * n + 2 * 1500 * n * 3 * n
@@ -161,6 +189,7 @@ def main():
     barrier(pg)
     model.ctx.sync()
     st0 = model.ctx.stats()
+    model.ctx.token_ms(reset=True)
     t0 = time.perf_counter()
     results = []
     for _ in range(args.steps):
@@ -186,18 +215,31 @@ def main():
     enc_windows = st1["encode_windows"] - st0["encode_windows"]
     ms_per_token = steps_ms / max(steps_done, 1)
 
-    # roofline of the dominant stage: the per-token decoder step (HBM-bound),
-    # timed live with HIP events on the context stream over a replay of the step graph
+    # p50 per-token decode ms: median over the timed region's decode_steps chunks
+    tok = model.ctx.token_ms()
+    p50_token_ms = float(np.median(tok)) if len(tok) else ms_per_token
+
+    # roofline of the dominant kernel (k_gemv_x: the split-K projection GEMVs of the
+    # decoder step, ~35% of step time), timed live with HIP events on the context's
+    # stream over launches at the bench batch (all layers, so weights stream from HBM)
     n_win = min(args.max_windows, n_clips)
     model.ctx.encode([3000 * i for i in range(n_win)], [3000] * n_win)
     from whisper.decoding import DecodingTask
     task = DecodingTask(model, whisper.DecodingOptions(language="en", beam_size=args.beam))
     model.ctx.decode_begin(task.wh_opts(), [task.initial_tokens] * n_win, [task.sot_index] * n_win)
+    rows = n_win * args.beam
+    gemv_ms = model.ctx.time_stage(2, 3)
+    gemv_bytes = projection_bytes_per_launch(dims, rows)
+    xattn_ms = model.ctx.time_stage(3, 3)
+    xattn_bytes = cross_attn_bytes_per_launch(dims, n_win, rows)
     step_ms = model.ctx.time_stage(0, 20)
     mean_ctx = 3 + 112  # mid-window self-KV length for the byte count
     step_bytes = decoder_step_bytes(dims, n_win, args.beam, mean_ctx)
-    achieved = step_bytes / (step_ms * 1e-3) / 1e9
 
+    def gbs(b, ms):
+        return b / (ms * 1e-3) / 1e9
+
+    traffic = load_traffic("k_gemv_x")
     out = {
         "metric": "xRT (audio-s/s) large-v3 beam=5 @1/2/4/8 GPU; p50 per-token decode ms",
         "value": round(world * args.seconds * args.steps / elapsed_max, 3),
@@ -215,14 +257,24 @@ def main():
                                f"30 s clip grid, condition_on_previous_text=False, temperature=0",
                    "model": args.model, "global_batch": n_clips * world, "seq_len": 448,
                    "parallelism": f"windows sharded over {world} GPU(s), RCCL all-reduce(max)+gather"},
-        "p50_token_ms": round(ms_per_token, 4),
+        "p50_token_ms": round(p50_token_ms, 4),
+        "mean_token_ms": round(ms_per_token, 4),
         "tokens_per_window": round(gathered[0][1] / max(1, n_clips), 1),
         "encoder_ms_per_window": round(enc_ms / max(enc_windows, 1), 3),
         "encoder_tflops": round(encoder_flops(dims) * enc_windows / (enc_ms * 1e-3) / 1e12, 1) if enc_ms else None,
-        "roofline": {"bound": "hbm", "kernel": f"decoder step hipGraph ({n_win} windows x {args.beam} beams)",
-                     "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
-                     "bytes_per_launch": step_bytes, "ms_per_launch": round(step_ms, 4)},
+        "roofline": {"bound": "hbm", "kernel": f"k_gemv_x split-K projection GEMV ({rows} rows, avg of the six "
+                                                f"per decoder layer)",
+                     "achieved": round(gbs(gemv_bytes, gemv_ms), 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(gbs(gemv_bytes, gemv_ms) / HBM_PEAK_GBS, 4),
+                     "traffic": traffic, "bytes_per_launch": gemv_bytes, "ms_per_launch": round(gemv_ms, 5)},
+        "roofline_cross_attn": {"bound": "hbm", "kernel": f"k_cross_attn ({n_win} windows x {args.beam} beams)",
+                                "achieved": round(gbs(xattn_bytes, xattn_ms), 1), "peak": HBM_PEAK_GBS,
+                                "frac": round(gbs(xattn_bytes, xattn_ms) / HBM_PEAK_GBS, 4),
+                                "bytes_per_launch": xattn_bytes, "ms_per_launch": round(xattn_ms, 5)},
+        "roofline_step": {"bound": "hbm", "kernel": f"decoder step hipGraph ({n_win} windows x {args.beam} beams)",
+                          "achieved": round(gbs(step_bytes, step_ms), 1), "peak": HBM_PEAK_GBS,
+                          "frac": round(gbs(step_bytes, step_ms) / HBM_PEAK_GBS, 4),
+                          "bytes_per_launch": step_bytes, "ms_per_launch": round(step_ms, 4)},
     }
     if rank == 0 and world == 1 and args.cpu_baseline and sd is not None:
         try:

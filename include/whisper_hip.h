@@ -82,11 +82,18 @@ int wh_set_mel_filters(wh_ctx* ctx, int n_mels, const float* filters);
    normalize = 1 applies the global-max floor and scaling immediately. */
 int wh_log_mel(wh_ctx* ctx, const float* audio, int64_t n_samples, int64_t padding, int n_mels, int normalize,
                int64_t* n_frames);
+/* frames [frame0, frame0 + count) of the same log-mel (count < 0: to the end); the
+   context stores them with their absolute offset, so wh_encode seeks and wh_mel_read
+   frames stay absolute.  One rank of a file sharded over GPUs computes only the frames
+   of its clips; the global max (wh_mel_max) is then all-reduced and applied with
+   wh_mel_normalize.  *total_frames = (n + padding) / 160. */
+int wh_log_mel_frames(wh_ctx* ctx, const float* audio, int64_t n_samples, int64_t padding, int n_mels,
+                      int64_t frame0, int64_t count, int normalize, int64_t* total_frames);
 /* keep audio resident in HBM; wh_log_mel(ctx, NULL, n, ...) then computes from it */
 int wh_audio_upload(wh_ctx* ctx, const float* audio, int64_t n_samples);
 int wh_mel_max(wh_ctx* ctx, float* gmax);              /* raw log10 max of the last wh_log_mel */
 int wh_mel_normalize(wh_ctx* ctx, float gmax);         /* floor at gmax-8, (x+4)/4 */
-int wh_mel_read(wh_ctx* ctx, float* out, int64_t frame0, int64_t n_frames); /* [n_mels][n_frames] */
+int wh_mel_read(wh_ctx* ctx, float* out, int64_t frame0, int64_t n_frames); /* [n_mels][n_frames], absolute frames */
 int wh_mel_write(wh_ctx* ctx, const float* mel, int64_t n_frames);          /* host mel -> context */
 
 /* encoder + cross-KV for n_win windows of the context mel: window i = frames
@@ -119,9 +126,18 @@ int wh_prefill_logits(wh_ctx* ctx, int slot, const int* tokens, int n_tokens, fl
 int wh_stats(wh_ctx* ctx, double* out, int n);
 int wh_sync(wh_ctx* ctx);
 
+/* per-token wall milliseconds of every decode_steps chunk since the last reset
+   (chunk wall time / steps in the chunk, host poll included): *n = count, up to
+   cap values copied to out (nullable); reset != 0 clears the record.  Feeds the
+   p50 per-token decode ms of BASELINE.json's metric. */
+int wh_token_ms(wh_ctx* ctx, float* out, int cap, int* n, int reset);
+
 /* timing of the dominant kernels for roofline reporting: runs `iters` launches of
    the given stage on the context's own stream between HIP events.
-   what: 0 = one decoder step graph (current batch), 1 = encoder of 1 window */
+   what: 0 = one decoder step graph (current batch), 1 = encoder of 1 window,
+         2 = one split-K projection GEMV launch (k_gemv_x; the six per layer, all layers),
+         3 = one cross-attention launch (k_cross_attn, all layers).
+   For 2 and 3 *ms_per_iter is the average duration of a single kernel launch. */
 int wh_time_stage(wh_ctx* ctx, int what, int iters, double* ms_per_iter);
 
 #ifdef __cplusplus

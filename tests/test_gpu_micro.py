@@ -100,8 +100,11 @@ def test_decode_tokens(micro, window_mel, key, opts):
         assert agree >= 1
 
 
-@pytest.mark.parametrize("run", ["clip_beam", "clip_greedy", "seq_greedy"])
-def test_transcribe_segments(micro, run):
+@pytest.mark.parametrize("run,schedule", [("clip_beam", "auto"), ("clip_greedy", "auto"), ("seq_greedy", "auto"),
+                                          ("clip_beam", "sequential"), ("clip_greedy", "sequential")])
+def test_transcribe_segments(micro, run, schedule):
+    """clip runs under "auto" take the batched schedule (all clips' windows through
+    the encoder and step graph together); "sequential" is the reference's loop."""
     import whisper
     from whisper import synthetic as S
     m, dt = micro
@@ -111,9 +114,35 @@ def test_transcribe_segments(micro, run):
         gt = json.load(f)
     kw = dict(gt["runs"][run])
     audio = S.synthetic_audio(gt["audio_seconds"], seed=gt["audio_seed"])
-    out = whisper.transcribe(m, audio, temperature=0.0, language="en", **kw)
+    out = whisper.transcribe(m, audio, temperature=0.0, language="en", schedule=schedule, **kw)
     ref = gt["segments"][run]
     assert [s["tokens"] for s in out["segments"]] == [s["tokens"] for s in ref]
     assert [s["seek"] for s in out["segments"]] == [s["seek"] for s in ref]
     for a, b in zip(out["segments"], ref):
         assert a["start"] == pytest.approx(b["start"]) and a["end"] == pytest.approx(b["end"])
+
+
+@pytest.mark.parametrize("run", ["clip_greedy", "clip_beam"])
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_replay_equals_reference(micro, run, world):
+    """whisper/distributed.py on one GPU: every rank's phase 1 (its mel frames +
+    local max), the MAX reduction, then each rank's phase 2 in turn; the merged
+    segments must equal the reference transcribe() of the whole file."""
+    from whisper import distributed as D
+    from whisper import synthetic as S
+    m, dt = micro
+    if dt != "fp32":
+        pytest.skip("segment-exact parity is an fp32 claim")
+    with open(os.path.join(GOLDEN, "micro_transcribe.json")) as f:
+        gt = json.load(f)
+    kw = dict(gt["runs"][run])
+    kw.pop("clip_timestamps"), kw.pop("condition_on_previous_text", None)
+    audio = S.synthetic_audio(gt["audio_seconds"], seed=gt["audio_seed"])
+    states = [D.prepare_shard(m, audio, r, world) for r in range(world)]
+    g = max(s.local_max for s in states)
+    per_rank = [D.run_shard(m, s, g, audio=audio, temperature=0.0, language="en", **kw) for s in states]
+    merged = D.merge_segments(per_rank)
+    ref = gt["segments"][run]
+    assert [s["tokens"] for s in merged] == [s["tokens"] for s in ref]
+    assert [s["seek"] for s in merged] == [s["seek"] for s in ref]
+    assert [s["id"] for s in merged] == list(range(len(ref)))

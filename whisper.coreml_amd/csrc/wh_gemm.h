@@ -42,6 +42,7 @@ struct GemmArgs {
   // skinny GEMM only: row gather (X row of output row m = x_rows[m]) and split-K
   const int* x_rows = nullptr;
   int ksplit = 1;
+  int mt_block = 0;  // 16-row tiles per block (0 = min(ceil(M/16), 8))
 };
 
 template <typename T, int EPI>
@@ -96,6 +97,6 @@ template <typename T>
 int launch_gemm(const GemmArgs& a, int epi, hipStream_t st);
 
 // split-K factor the skinny paths use for EPI_PARTIAL at this shape (<= min(16, max_z))
-int gemv_ksplit(int M, int N, int K, int max_z = 16);
+int gemv_ksplit(int M, int N, int K, int max_z = 16, int mt_block = 0);
 
 }  // namespace wh

@@ -16,6 +16,9 @@
 // consecutive output columns of one row (wide epilogue stores).
 #include "wh_gemm.h"
 
+#include <algorithm>
+#include <cstdlib>
+
 namespace wh {
 
 // ============================================================ big tile GEMM
@@ -143,19 +146,21 @@ __global__ __launch_bounds__(512) void k_gemv_rows(GemmArgs a) {
   const T* X = reinterpret_cast<const T*>(a.X);
   const T* W = reinterpret_cast<const T*>(a.W);
 
-  // split-K: blockIdx.z owns k in [kz*Kc, (kz+1)*Kc)
+  // split-K: blockIdx.z owns the 32-wide k-steps [S*kz/Z, S*(kz+1)/Z)
   const int kz = blockIdx.z;
-  const int Kc = a.K / gridDim.z;
+  const int S = a.K / 32;
+  const int kb = (S * kz / (int)gridDim.z) * 32;
+  const int Kc = (S * (kz + 1) / (int)gridDim.z) * 32 - kb;
   int nrow = n0 + r;
   if (nrow >= a.N) nrow = a.N - 1;
-  const T* wp = W + (int64_t)nrow * a.K + (int64_t)kz * Kc + 8 * g;
+  const T* wp = W + (int64_t)nrow * a.K + kb + 8 * g;
   const T* xp[MT];
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt) {
     int m = mb + mt * 16 + r;
     if (m >= a.M) m = a.M - 1;
     const int xr = a.x_rows ? a.x_rows[m] : m;
-    xp[mt] = X + (int64_t)xr * a.ldx + (int64_t)kz * Kc + 8 * g;
+    xp[mt] = X + (int64_t)xr * a.ldx + kb + 8 * g;
   }
   float4_t acc[MT];
 #pragma unroll
@@ -230,8 +235,9 @@ __global__ __launch_bounds__(256) void k_gemv_x(GemmArgs a) {
   const int n0 = blockIdx.x * 64 + wave * 16;
   const int mb = blockIdx.y * (16 * MT);
   const int kz = blockIdx.z;
-  const int Kc = a.K / gridDim.z;
-  const int kbase = kz * Kc;
+  const int S = a.K / 32;
+  const int kbase = (S * kz / (int)gridDim.z) * 32;
+  const int Kc = (S * (kz + 1) / (int)gridDim.z) * 32 - kbase;
   const T* X = reinterpret_cast<const T*>(a.X);
   const T* W = reinterpret_cast<const T*>(a.W);
   int nrow = n0 + r;
@@ -315,17 +321,27 @@ __global__ __launch_bounds__(256) void k_gemv_x(GemmArgs a) {
   }
 }
 
-int gemv_ksplit(int M, int N, int K, int max_z) {
-  // split-K for the residual projections: enough workgroups to cover the CUs,
-  // a divisor of the 32-wide step count, at most 16 slabs
+static int rows_per_block(int M, int mt_block) {
+  const int mt = (M + 15) / 16;
+  if (mt_block > 0) return std::min(mt_block, std::min(mt, 8));
+  return mt >= 8 ? 8 : mt;
+}
+
+int gemv_ksplit(int M, int N, int K, int max_z, int mt_block) {
+  // split-K for the skinny paths.  One block's latency is nearly independent of its
+  // k-range at these sizes, so the wall time is one block's latency as long as the
+  // blocks fit on the CUs at once: take the largest z with blocks <= the target
+  // (default 256 = one per CU; WHISPER_HIP_GEMV_WGS overrides for tuning).
+  const char* env = getenv("WHISPER_HIP_GEMV_WGS");
+  const int target = env ? atoi(env) : 256;
   const int mt = (M + 15) / 16;
   const bool xpath = mt >= 3;  // k_gemv_x (EPI_PARTIAL with >= 33 rows)
-  const int rows_per = xpath ? (mt >= 8 ? 8 : mt) : (mt >= 8 ? 8 : mt);
-  const int wgs = (xpath ? (N + 63) / 64 : (N + 15) / 16) * ((M + 16 * rows_per - 1) / (16 * rows_per));
+  const int rp = rows_per_block(M, mt_block);
+  const int wgs = (xpath ? (N + 63) / 64 : (N + 15) / 16) * ((M + 16 * rp - 1) / (16 * rp));
   const int steps = K / 32;
   int best = 1;
-  for (int z = 1; z <= 16 && z <= max_z; ++z)
-    if (steps % z == 0 && wgs * z <= 320) best = z;
+  for (int z = 1; z <= 16 && z <= max_z && z <= steps; ++z)
+    if (wgs * z <= target) best = z;
   return best;
 }
 
@@ -347,9 +363,9 @@ int launch_gemm(const GemmArgs& a, int epi, hipStream_t st) {
     if (a.K % 32) return -2;
     if (a.x_group_rows != a.M && a.x_group_rows != 0 && a.x_group_rows < a.M) return -3;  // skinny: plain rows only
     const int mt = (a.M + 15) / 16;
-    const int rows_per = mt >= 8 ? 8 : mt;
+    const int rows_per = rows_per_block(a.M, a.mt_block);
     const int ks = epi == EPI_PARTIAL ? a.ksplit : 1;
-    if (ks < 1 || a.K % (32 * ks)) return -4;
+    if (ks < 1 || ks > a.K / 32) return -4;
     if (mt >= 3 && (epi == EPI_PARTIAL || (a.N + 63) / 64 >= 70)) {  // tall-skinny: X shared via LDS by 4 column tiles
       dim3 gx((a.N + 63) / 64, (a.M + 16 * rows_per - 1) / (16 * rows_per), ks);
 #define LAUNCHX(MT_)                                                                            \

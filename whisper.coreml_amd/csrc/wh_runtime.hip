@@ -6,6 +6,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -14,6 +15,7 @@
 #include <set>
 #include <string>
 #include <vector>
+#include <chrono>
 
 #include "whisper_hip.h"
 #include "wh_gemm.h"
@@ -89,6 +91,8 @@ struct wh_ctx {
   virtual int load(const std::string& name, const float* data, const int64_t* shape, int ndim) = 0;
   virtual int finalize() = 0;
   virtual int log_mel(const float* audio, int64_t n, int64_t pad, int n_mels, int normalize, int64_t* nf) = 0;
+  virtual int log_mel_frames(const float* audio, int64_t n, int64_t pad, int n_mels, int64_t frame0, int64_t count,
+                             int normalize, int64_t* total_frames) = 0;
   virtual int audio_upload(const float* audio, int64_t n) = 0;
   virtual int mel_max(float* g) = 0;
   virtual int mel_normalize(float g) = 0;
@@ -104,6 +108,7 @@ struct wh_ctx {
                           float* fin_score, float* nsp) = 0;
   virtual int prefill_logits(int slot, const int* tokens, int n, float* logits, const int* ah, int na, float* aqk) = 0;
   virtual int time_stage(int what, int iters, double* ms) = 0;
+  std::vector<float> token_ms;  // per-token wall ms of each decode_steps chunk
   double stats[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   int maxc = 5;
   int maxc_stride = 1;
@@ -138,6 +143,8 @@ struct Ctx : public wh_ctx {
   float* d_mel = nullptr;
   size_t mel_cap = 0;
   int64_t mel_frames = 0;
+  int64_t mel_f0 = 0;  // absolute index of the first stored frame
+  std::vector<int64_t> h_seeks;
   int mel_nm = 0;
   unsigned* d_gmax = nullptr;
   float* d_gmax_f = nullptr;
@@ -462,16 +469,28 @@ struct Ctx : public wh_ctx {
   }
   // audio == nullptr: use the resident buffer of wh_audio_upload (n must match)
   int log_mel(const float* audio, int64_t n, int64_t pad, int n_mels, int normalize, int64_t* nf) override {
+    int64_t total = 0;
+    TRY(log_mel_frames(audio, n, pad, n_mels, 0, -1, normalize, &total));
+    *nf = total;
+    return 0;
+  }
+  // frames [frame0, frame0 + count) of the padded signal's log-mel (count < 0: to the
+  // end); the context keeps them with their absolute frame offset (mel_f0), so window
+  // seeks stay absolute.  A rank of a sharded file computes only its own frames.
+  int log_mel_frames(const float* audio, int64_t n, int64_t pad, int n_mels, int64_t frame0, int64_t count,
+                     int normalize, int64_t* total_frames) override {
     if (!h_filters.count(n_mels)) return fail(-7, "mel filters for n_mels=" + std::to_string(n_mels) + " not set");
-    if (n + pad <= 200) return fail(-7, "audio too short for reflect padding");
+    if (n + pad <= 200 || n < 1) return fail(-7, "audio too short for reflect padding");
     if (!audio && n != audio_n) return fail(-7, "no resident audio of that length");
-    const int64_t frames = (n + pad) / 160;
+    const int64_t total = (n + pad) / 160;
+    if (count < 0) count = total - frame0;
+    if (frame0 < 0 || count < 1 || frame0 + count > total) return fail(-7, "mel frame range out of bounds");
     if (audio && (size_t)n > audio_cap) {
       if (d_audio) hipFree(d_audio);
       audio_cap = std::max<size_t>(n, 16000);
       HIPCHK(hipMalloc(&d_audio, audio_cap * 4));
     }
-    const size_t need = (size_t)n_mels * frames;
+    const size_t need = (size_t)n_mels * count;
     if (need > mel_cap) {
       if (d_mel) hipFree(d_mel);
       mel_cap = need;
@@ -483,16 +502,17 @@ struct Ctx : public wh_ctx {
       audio_n = n;
     }
     HIPCHK(hipMemsetAsync(d_gmax, 0, 16, st));
-    launch_mel(d_audio, n, n + pad, 0, frames, d_filters[n_mels], n_mels, d_mel, frames, d_gmax, st);
-    if (normalize) launch_mel_norm(d_mel, frames, frames, n_mels, d_gmax, nullptr, st);
+    launch_mel(d_audio, n, n + pad, frame0, count, d_filters[n_mels], n_mels, d_mel, count, d_gmax, st);
+    if (normalize) launch_mel_norm(d_mel, count, count, n_mels, d_gmax, nullptr, st);
     hipEventRecord(tm.b, st);
     HIPCHK(hipStreamSynchronize(st));
     float ms = 0;
     hipEventElapsedTime(&ms, tm.a, tm.b);
     stats[0] += ms;
-    mel_frames = frames;
+    mel_frames = count;
+    mel_f0 = frame0;
     mel_nm = n_mels;
-    *nf = frames;
+    *total_frames = total;
     return 0;
   }
   std::map<int, std::vector<float>> h_filters;
@@ -510,7 +530,8 @@ struct Ctx : public wh_ctx {
     return 0;
   }
   int mel_read(float* out, int64_t f0, int64_t nf) override {
-    if (f0 < 0 || f0 + nf > mel_frames) return fail(-8, "mel_read out of range");
+    f0 -= mel_f0;  // absolute frame -> stored frame
+    if (f0 < 0 || nf < 0 || f0 + nf > mel_frames) return fail(-8, "mel_read out of range");
     HIPCHK(hipMemcpy2D(out, nf * 4, d_mel + f0, mel_frames * 4, nf * 4, mel_nm, hipMemcpyDeviceToHost));
     return 0;
   }
@@ -523,6 +544,7 @@ struct Ctx : public wh_ctx {
     }
     HIPCHK(hipMemcpy(d_mel, mel, need * 4, hipMemcpyHostToDevice));
     mel_frames = nf;
+    mel_f0 = 0;
     mel_nm = nm;
     return 0;
   }
@@ -572,10 +594,15 @@ struct Ctx : public wh_ctx {
     if (!finalized) return fail(-9, "weights not finalized");
     if (n_win < 1 || n_win > Wcap) return fail(-9, "n_win out of range");
     if (!d_mel || mel_nm != nm) return fail(-9, "no mel of the model's n_mels in the context");
-    for (int i = 0; i < n_win; ++i)
-      if (seeks[i] < 0 || seeks[i] >= mel_frames || segs[i] < 1) return fail(-9, "bad window");
+    // seeks are absolute frames; the stored mel starts at mel_f0
+    h_seeks.resize(n_win);
+    for (int i = 0; i < n_win; ++i) {
+      const int64_t s = seeks[i] - mel_f0;
+      if (s < 0 || segs[i] < 1 || s + std::min(segs[i], 3000) > mel_frames) return fail(-9, "bad window");
+      h_seeks[i] = s;
+    }
     hipEventRecord(tm.a, st);
-    HIPCHK(hipMemcpyAsync(d_seeks, seeks, n_win * 8, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(d_seeks, h_seeks.data(), n_win * 8, hipMemcpyHostToDevice, st));
     HIPCHK(hipMemcpyAsync(d_segs, segs, n_win * 4, hipMemcpyHostToDevice, st));
     const int WE = std::min(Wcap, ENC_CHUNK);
     for (int s0 = 0; s0 < n_win; s0 += WE) TRY(encode_chunk(s0, std::min(WE, n_win - s0)));
@@ -901,12 +928,17 @@ struct Ctx : public wh_ctx {
     hipEventRecord(tm.a, st);
     int steps = 0, done = 0;
     const int chunk = 8;
+    auto tc = std::chrono::steady_clock::now();
     while (steps < max_steps) {
       const int k = std::min(chunk, max_steps - steps);
       for (int i = 0; i < k; ++i) TRY(launch_step());
       steps += k;
       HIPCHK(hipMemcpyAsync(h_done, S.done, cur_nwin * 4, hipMemcpyDeviceToHost, st));
       HIPCHK(hipStreamSynchronize(st));
+      // per-token wall time of this chunk (graph launches + done poll), for the p50
+      const auto now = std::chrono::steady_clock::now();
+      token_ms.push_back((float)(std::chrono::duration<double, std::milli>(now - tc).count() / k));
+      tc = now;
       done = 0;
       for (int w = 0; w < cur_nwin; ++w) done += h_done[w] != 0;
       if (done == cur_nwin) break;
@@ -995,10 +1027,48 @@ struct Ctx : public wh_ctx {
       hipEventRecord(tm.a, st);
       for (int i = 0; i < iters; ++i) TRY(launch_step());
       hipEventRecord(tm.b, st);
-    } else {
+    } else if (what == 1) {
       hipEventRecord(tm.a, st);
       for (int i = 0; i < iters; ++i) TRY(encode_chunk(0, 1));
       hipEventRecord(tm.b, st);
+    } else if (what == 2 || what == 3) {
+      // per-launch time of one decoder-step kernel at the current batch, over all
+      // layers (so weights / cross-KV stream from HBM as in the step, not from cache):
+      // 2 = the six split-K projection GEMVs of each layer (k_gemv_x, EPI_PARTIAL),
+      // 3 = k_cross_attn
+      if (cur_nwin < 1) return fail(-16, "no decode batch");
+      const int R = cur_nwin * cur_G, n = ns;
+      int launches = 0;
+      hipEventRecord(tm.a, st);
+      for (int i = 0; i < iters; ++i)
+        for (int l = 0; l < Ld; ++l) {
+          auto& e = dec[l];
+          if (what == 2) {
+            struct P { const T* X; int K; const T* W; int N; } ps[6] = {
+                {xn_d, n, e.wqkv, 3 * n}, {att_d, n, e.wo, n}, {xn_d, n, e.wqx, n},
+                {att_d, n, e.wox, n},     {xn_d, n, e.w1, 4 * n}, {hm_d, 4 * n, e.w2, n}};
+            for (auto& p : ps) {
+              GemmArgs g;
+              g.out_f32 = part; g.ldo = p.N; g.ksplit = gemv_ksplit(R, p.N, p.K, part_slabs(R, p.N));
+              TRY(gemm(p.X, p.K, p.W, nullptr, R, p.N, p.K, EPI_PARTIAL, g));
+              ++launches;
+            }
+          } else {
+            const T* ck = ckv + (size_t)(2 * l) * Wcap * TKP * n;
+            const T* cv = ckv + (size_t)(2 * l + 1) * Wcap * TKP * n;
+            launch_cross_attn<T>(q_d, n, ck, cv, 1500, nh, NSPLIT, cur_nwin, st_win_row0, st_win_nrows, st_win_slot,
+                                 (int64_t)TKP * n, po, pm, pl, att_d, n, R, nullptr, nullptr, 0, st);
+            ++launches;
+          }
+        }
+      hipEventRecord(tm.b, st);
+      HIPCHK(hipStreamSynchronize(st));
+      float t = 0;
+      hipEventElapsedTime(&t, tm.a, tm.b);
+      *ms = t / launches;
+      return 0;
+    } else {
+      return fail(-2, "time_stage: unknown stage");
     }
     HIPCHK(hipStreamSynchronize(st));
     float t = 0;
@@ -1076,8 +1146,21 @@ int wh_load_tensor(wh_ctx* ctx, const char* name, const float* data, const int64
   CTXCALL(ctx->load(name, data, shape, ndim));
 }
 int wh_finalize(wh_ctx* ctx) { CTXCALL(ctx->finalize()); }
+int wh_token_ms(wh_ctx* ctx, float* out, int cap, int* n, int reset) {
+  if (!ctx) return -1;
+  const int cnt = (int)ctx->token_ms.size();
+  if (n) *n = cnt;
+  if (out)
+    for (int i = 0; i < cnt && i < cap; ++i) out[i] = ctx->token_ms[i];
+  if (reset) ctx->token_ms.clear();
+  return 0;
+}
 int wh_log_mel(wh_ctx* ctx, const float* audio, int64_t n, int64_t pad, int n_mels, int normalize, int64_t* nf) {
   CTXCALL(ctx->log_mel(audio, n, pad, n_mels, normalize, nf));
+}
+int wh_log_mel_frames(wh_ctx* ctx, const float* audio, int64_t n, int64_t pad, int n_mels, int64_t frame0,
+                      int64_t count, int normalize, int64_t* total_frames) {
+  CTXCALL(ctx->log_mel_frames(audio, n, pad, n_mels, frame0, count, normalize, total_frames));
 }
 int wh_audio_upload(wh_ctx* ctx, const float* audio, int64_t n) {
   if (!audio || n <= 0) return fail(-1, "bad audio");

@@ -51,6 +51,8 @@ _EXPORTS = {
     "wh_finalize": (c_int, [c_void_p]),
     "wh_set_mel_filters": (c_int, [c_void_p, c_int, c_void_p]),
     "wh_log_mel": (c_int, [c_void_p, c_void_p, c_int64, c_int64, c_int, c_int, POINTER(c_int64)]),
+    "wh_log_mel_frames": (c_int, [c_void_p, c_void_p, c_int64, c_int64, c_int, c_int64, c_int64, c_int,
+                                  POINTER(c_int64)]),
     "wh_audio_upload": (c_int, [c_void_p, c_void_p, c_int64]),
     "wh_mel_max": (c_int, [c_void_p, POINTER(c_float)]),
     "wh_mel_normalize": (c_int, [c_void_p, c_float]),
@@ -68,6 +70,7 @@ _EXPORTS = {
     "wh_stats": (c_int, [c_void_p, POINTER(c_double), c_int]),
     "wh_sync": (c_int, [c_void_p]),
     "wh_time_stage": (c_int, [c_void_p, c_int, c_int, POINTER(c_double)]),
+    "wh_token_ms": (c_int, [c_void_p, c_void_p, c_int, POINTER(c_int), c_int]),
 }
 
 
@@ -173,6 +176,17 @@ class HipContext:
                                         ctypes.byref(nf)), "wh_log_mel")
         return nf.value
 
+    def log_mel_frames(self, audio: Optional[np.ndarray], n_samples: int, n_mels: int, frame0: int, count: int,
+                       padding: int = 0, normalize: bool = True) -> int:
+        """Frames [frame0, frame0+count) of the padded file's log-mel (audio None: the
+        resident buffer).  Returns the whole file's frame count."""
+        a = None if audio is None else np.ascontiguousarray(audio, dtype=np.float32)
+        tot = c_int64()
+        self._check(self.lib.wh_log_mel_frames(self.h, None if a is None else _ptr(a), int(n_samples), int(padding),
+                                               n_mels, int(frame0), int(count), int(normalize), ctypes.byref(tot)),
+                    "wh_log_mel_frames")
+        return tot.value
+
     def mel_max(self) -> float:
         g = c_float()
         self._check(self.lib.wh_mel_max(self.h, ctypes.byref(g)), "wh_mel_max")
@@ -261,6 +275,14 @@ class HipContext:
 
     def sync(self):
         self._check(self.lib.wh_sync(self.h), "wh_sync")
+
+    def token_ms(self, reset: bool = False) -> np.ndarray:
+        """Per-token wall ms of each decode_steps chunk since the last reset."""
+        n = c_int(0)
+        self._check(self.lib.wh_token_ms(self.h, None, 0, ctypes.byref(n), 0), "wh_token_ms")
+        out = np.zeros(max(n.value, 1), np.float32)
+        self._check(self.lib.wh_token_ms(self.h, _ptr(out), n.value, ctypes.byref(n), int(reset)), "wh_token_ms")
+        return out[:n.value]
 
     def time_stage(self, what: int, iters: int) -> float:
         ms = c_double()

@@ -124,7 +124,8 @@ def transcribe(model: "Whisper", audio: Union[str, np.ndarray], *, verbose: Opti
                word_timestamps: bool = False, prepend_punctuations: str = "\"'“¿([{-",
                append_punctuations: str = "\"'.。,，!！?？:：”)]}、", clip_timestamps: Union[str, List[float]] = "0",
                hallucination_silence_threshold: Optional[float] = None, schedule: str = "auto",
-               mel_max_reduce=None, **decode_options) -> dict:
+               mel_max_reduce=None, _mel_prepared: Optional[Tuple[int, int, int]] = None,
+               **decode_options) -> dict:
     """transcribe.py:41-524.  Extra keywords: ``schedule`` ("auto", "sequential",
     "batched") and ``mel_max_reduce`` (callable local max -> global max, used when
     one file is sharded over GPUs: the log-mel floor is a whole-file max,
@@ -136,7 +137,16 @@ def transcribe(model: "Whisper", audio: Union[str, np.ndarray], *, verbose: Opti
     decode_options.pop("fp16", None)
     ctx = model.ctx
     n_mels = model.dims.n_mels
-    if isinstance(audio, DeviceAudio):
+    if _mel_prepared is not None:
+        # distributed.run_shard: this rank's frames are already in the context and
+        # normalised with the all-reduced max; seeks stay absolute
+        if decode_options.get("language") is None:
+            raise ValueError("sharded transcription needs an explicit language")
+
+        def compute_mel():
+            return _mel_prepared[0]
+        mel_max_reduce = None
+    elif isinstance(audio, DeviceAudio):
         if audio.ctx is not ctx:
             raise ValueError("DeviceAudio belongs to another model context")
         resident = audio.n_samples
@@ -154,7 +164,7 @@ def transcribe(model: "Whisper", audio: Union[str, np.ndarray], *, verbose: Opti
 
     def prepare_mel():
         nf = compute_mel()
-        if mel_max_reduce is not None:
+        if mel_max_reduce is not None and _mel_prepared is None:
             ctx.mel_normalize(float(mel_max_reduce(ctx.mel_max())))
         return nf
 
@@ -200,7 +210,8 @@ def transcribe(model: "Whisper", audio: Union[str, np.ndarray], *, verbose: Opti
     initial_prompt_tokens = list(initial_prompt) if initial_prompt else []
 
     batched = schedule == "batched" or (
-        schedule == "auto" and not condition_on_previous_text and not carry_initial_prompt and len(seek_clips) > 1)
+        schedule == "auto" and not condition_on_previous_text and not carry_initial_prompt
+        and not initial_prompt_tokens and len(seek_clips) > 1)
     state = dict(content_frames=content_frames, tokenizer=tokenizer, temperatures=temperatures,
                  thresholds=thresholds, base=base, input_stride=input_stride, time_precision=time_precision)
     if batched:
