@@ -43,6 +43,11 @@ struct GemmArgs {
   const int* x_rows = nullptr;
   int ksplit = 1;
   int mt_block = 0;  // 16-row tiles per block (0 = min(ceil(M/16), 8))
+  // k_proj PRO_LN prologue: X = LayerNorm(xf32 rows; ln_g, ln_b, ln_eps)
+  const float* xf32 = nullptr;
+  const float* ln_g = nullptr;
+  const float* ln_b = nullptr;
+  float ln_eps = 1e-5f;
 };
 
 template <typename T, int EPI>
@@ -95,6 +100,12 @@ WH_DEV void epilogue_store(const GemmArgs& a, int m, int gi, int ri, int n, floa
 
 template <typename T>
 int launch_gemm(const GemmArgs& a, int epi, hipStream_t st);
+
+// decoder-step projections (k_proj, wh_proj.hip) into split-K partial slabs
+// out_f32[z][M][N]; returns 0 and the split count, or < 0 when no tile configuration
+// fits the shape (callers then use launch_gemm's EPI_PARTIAL path)
+template <typename T>
+int launch_proj_partial(const GemmArgs& a, int max_z, hipStream_t st, int* z_out);
 
 // split-K factor the skinny paths use for EPI_PARTIAL at this shape (<= min(16, max_z))
 int gemv_ksplit(int M, int N, int K, int max_z = 16, int mt_block = 0);

@@ -654,6 +654,22 @@ struct Ctx : public wh_ctx {
   // how many [R][N] fp32 slabs fit in the partial buffer
   int part_slabs(int R, int N) const { return (int)std::min<int64_t>(16, (int64_t)RSPLIT * RD * ns / ((int64_t)R * N)); }
 
+  // X[R][K] W^T into the split-K partial slabs part[z][R][N]: k_proj where a tile
+  // configuration fits (decode rows <= 112), the k_gemv path otherwise; *ks = z
+  int partial(const void* X, int ldx, const T* W, int R, int N, int K, int* ks) {
+    GemmArgs g;
+    g.X = X; g.ldx = ldx; g.W = W; g.M = R; g.N = N; g.K = K; g.x_group_rows = R;
+    g.out_f32 = part; g.ldo = N;
+    const int maxz = part_slabs(R, N);
+    const int rc = launch_proj_partial<T>(g, maxz, st, ks);
+    if (rc == 0) return 0;
+    if (rc != -1) return fail(-20, "k_proj launch failed code " + std::to_string(rc));
+    *ks = gemv_ksplit(R, N, K, maxz);
+    g = GemmArgs();
+    g.out_f32 = part; g.ldo = N; g.ksplit = *ks;
+    return gemm(X, ldx, W, nullptr, R, N, K, EPI_PARTIAL, g);
+  }
+
   int resid(const T* X, int K, const T* W, const float* b, int R, const float* lg, const float* lb) {
     const int n = ns;
     GemmArgs g;
@@ -662,9 +678,8 @@ struct Ctx : public wh_ctx {
       TRY(gemm(X, K, W, b, R, n, K, EPI_RESID, g));
       launch_resid_ln<T>(x_d, nullptr, 0, 0, nullptr, xn_d, lg, lb, R, n, 1e-5f, st);
     } else {
-      const int ks = gemv_ksplit(R, n, K, part_slabs(R, n));
-      g.out_f32 = part; g.ldo = n; g.ksplit = ks;
-      TRY(gemm(X, K, W, nullptr, R, n, K, EPI_PARTIAL, g));
+      int ks = 0;
+      TRY(partial(X, K, W, R, n, K, &ks));
       launch_resid_ln<T>(x_d, part, ks, (int64_t)R * n, b, xn_d, lg, lb, R, n, 1e-5f, st);
     }
     return 0;
@@ -675,9 +690,8 @@ struct Ctx : public wh_ctx {
   int proj(const T* W, const float* b, int R, int N, T* out, int gelu, bool skinny) {
     GemmArgs g;
     if (skinny) {
-      const int ks = gemv_ksplit(R, N, ns, part_slabs(R, N));
-      g.out_f32 = part; g.ldo = N; g.ksplit = ks;
-      TRY(gemm(xn_d, ns, W, nullptr, R, N, ns, EPI_PARTIAL, g));
+      int ks = 0;
+      TRY(partial(xn_d, ns, W, R, N, ns, &ks));
       launch_reduce_store<T>(part, ks, (int64_t)R * N, b, out, N, R, N, gelu, st);
     } else {
       g.out = out; g.ldo = N;
@@ -699,9 +713,8 @@ struct Ctx : public wh_ctx {
     for (int l = 0; l < Ld; ++l) {
       auto& e = dec[l];
       if (skinny) {
-        const int ks = gemv_ksplit(R, 3 * n, n, part_slabs(R, 3 * n));
-        g = GemmArgs(); g.out_f32 = part; g.ldo = 3 * n; g.ksplit = ks;
-        TRY(gemm(xn_d, n, e.wqkv, nullptr, R, 3 * n, n, EPI_PARTIAL, g));
+        int ks = 0;
+        TRY(partial(xn_d, n, e.wqkv, R, 3 * n, n, &ks));
         launch_self_attn_qkv<T>(part, ks, (int64_t)R * 3 * n, e.bqkv, n, kc[l], vc[l], rw, rs, rp, S.anc, ancG, Gcap,
                                 nh, CTX, att_d, n, R, st);
       } else {
@@ -1048,9 +1061,8 @@ struct Ctx : public wh_ctx {
                 {xn_d, n, e.wqkv, 3 * n}, {att_d, n, e.wo, n}, {xn_d, n, e.wqx, n},
                 {att_d, n, e.wox, n},     {xn_d, n, e.w1, 4 * n}, {hm_d, 4 * n, e.w2, n}};
             for (auto& p : ps) {
-              GemmArgs g;
-              g.out_f32 = part; g.ldo = p.N; g.ksplit = gemv_ksplit(R, p.N, p.K, part_slabs(R, p.N));
-              TRY(gemm(p.X, p.K, p.W, nullptr, R, p.N, p.K, EPI_PARTIAL, g));
+              int ks = 0;
+              TRY(partial(p.X, p.K, p.W, R, p.N, p.K, &ks));
               ++launches;
             }
           } else {
