@@ -67,7 +67,7 @@ __device__ __forceinline__ unsigned long long splitmix64(unsigned long long z) {
   return z ^ (z >> 31);
 }
 
-__global__ __launch_bounds__(LR_THREADS) void k_logit_rows(const float* __restrict__ logits, int ldl, DecState s,
+__global__ __launch_bounds__(LR_THREADS) void k_logit_rows(float* __restrict__ logits, int ldl, DecState s,
                                                            DecOpts o) {
   __shared__ BlockRed sm;
   __shared__ int info[8];
@@ -108,21 +108,37 @@ __global__ __launch_bounds__(LR_THREADS) void k_logit_rows(const float* __restri
       if (o.max_initial >= 0) { mlo[nm] = tb + o.max_initial + 1; mhi[nm++] = V; }
     }
   }
-  const float* row = logits + (int64_t)r * ldl;
+  float* row = logits + (int64_t)r * ldl;
   const bool sb_first = first && o.suppress_blank;
-  // filtered logit i (re-read from L2 on every pass: the row does not fit registers)
-  auto val = [&](int i) -> float {
-    float v = row[i];
-    bool kill = false;
-    if (sb_first)
-      for (int b = 0; b < o.n_blank; ++b) kill |= (i == o.blank[b]);
-    if (o.suppress && ((o.suppress[i >> 5] >> (i & 31)) & 1u)) kill = true;
-    if (o.timestamps) {
-      kill |= (i == o.no_ts);
-      for (int q = 0; q < nm; ++q) kill |= (i >= mlo[q] && i < mhi[q]);
+  // the filters are applied once, in place (the logits are this step's scratch); every
+  // later pass re-reads the filtered row from L2 (it does not fit registers or LDS)
+  {
+    constexpr int U = 8;
+    for (int i0 = tid; i0 < V; i0 += LR_THREADS * U) {
+      float v[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int i = i0 + LR_THREADS * u;
+        v[u] = i < V ? row[i] : 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int i = i0 + LR_THREADS * u;
+        if (i >= V) continue;
+        bool kill = false;
+        if (sb_first)
+          for (int b = 0; b < o.n_blank; ++b) kill |= (i == o.blank[b]);
+        if (o.suppress && ((o.suppress[i >> 5] >> (i & 31)) & 1u)) kill = true;
+        if (o.timestamps) {
+          kill |= (i == o.no_ts);
+          for (int q = 0; q < nm; ++q) kill |= (i >= mlo[q] && i < mhi[q]);
+        }
+        if (kill) row[i] = -INFINITY;
+      }
     }
-    return kill ? -INFINITY : v;
-  };
+  }
+  __syncthreads();
+  auto val = [&](int i) -> float { return row[i]; };
   bool text_killed = false;
   if (o.timestamps) {
     // ApplyTimestampRules tail: if logsumexp(logprobs[tb:]) > max(logprobs[:tb]) mask text
@@ -191,9 +207,12 @@ __global__ __launch_bounds__(LR_THREADS) void k_logit_rows(const float* __restri
   int li[KC];
 #pragma unroll
   for (int q = 0; q < KC; ++q) { lv[q] = -INFINITY; li[q] = 0x7fffffff; }
+  float thr_v = -INFINITY;  // the thread's current need-th best (entry to beat)
+  int thr_i = 0x7fffffff;
   for (int i = tid; i < V; i += LR_THREADS) {
     float v = fval(i);
     int vi = i;
+    if (!better(v, vi, thr_v, thr_i)) continue;
 #pragma unroll
     for (int q = 0; q < KC; ++q) {
       if (q < need && better(v, vi, lv[q], li[q])) {
@@ -201,6 +220,9 @@ __global__ __launch_bounds__(LR_THREADS) void k_logit_rows(const float* __restri
         lv[q] = v; li[q] = vi; v = tv; vi = ti;
       }
     }
+#pragma unroll
+    for (int q = 0; q < KC; ++q)
+      if (q == need - 1) { thr_v = lv[q]; thr_i = li[q]; }
   }
   int head = 0;
   for (int q = 0; q < need; ++q) {
@@ -220,7 +242,7 @@ __global__ __launch_bounds__(LR_THREADS) void k_logit_rows(const float* __restri
   }
 }
 
-void launch_logit_rows(const float* logits, int ldl, const DecState& s, const DecOpts& o, int nwin, hipStream_t st) {
+void launch_logit_rows(float* logits, int ldl, const DecState& s, const DecOpts& o, int nwin, hipStream_t st) {
   k_logit_rows<<<nwin * s.G, LR_THREADS, 0, st>>>(logits, ldl, s, o);
 }
 

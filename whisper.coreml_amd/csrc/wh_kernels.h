@@ -77,7 +77,7 @@ struct DecOpts {
   unsigned long long seed;
 };
 
-void launch_logit_rows(const float* logits, int ldl, const DecState& s, const DecOpts& o, int nwin, hipStream_t st);
+void launch_logit_rows(float* logits, int ldl, const DecState& s, const DecOpts& o, int nwin, hipStream_t st);
 void launch_merge(const DecState& s, const DecOpts& o, int nwin, hipStream_t st);
 void launch_no_speech(const float* logits, int ldl, int rows, int V, int no_speech, float* out, hipStream_t st);
 void launch_broadcast_rows(const float* src, int ld_src, const int* src_rows, float* dst, int ld_dst, int G, int nwin,
