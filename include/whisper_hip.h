@@ -121,6 +121,22 @@ int wh_decode_maxc(wh_ctx* ctx);
 int wh_prefill_logits(wh_ctx* ctx, int slot, const int* tokens, int n_tokens, float* logits, const int* align_heads,
                       int n_align, float* align_qk);
 
+/* find_alignment's numeric half (reference whisper/timing.py:163-231), replacing the
+   model(tokens) first pass with cross-QK capture (model.py:110-119, decoder.py:306-313,
+   the decoder256 CoreML call of coreml.h:17-18 with out_cross_head_weights), the
+   softmax / z-norm / median filter / head mean (timing.py:197-205) and dtw
+   (timing.py:139-151, dtw_cpu :82-105 + backtrace :57-79) — all on the GPU.
+   tokens = sot_sequence (n_sot ids) + [no_timestamps] + text (T ids) + [eot]
+   (timing.py:175-182); the window's audio features must be in `slot`.
+   token_probs [T] = softmax(logits[n_sot + k][:eot])[text[k]] (timing.py:187-191);
+   path [2][T + 1 + num_frames/2]: text indices then time indices, *path_len valid
+   entries of each (the rows of dtw(-matrix), timing.py:206). */
+int wh_align(wh_ctx* ctx, int slot, const int* tokens, int n_tokens, int n_sot, int num_frames, const int* align_heads,
+             int n_align, int medfilt_width, float* token_probs, int* path, int* path_len);
+/* timing.dtw(x) of a host matrix x [n_rows][n_cols] (n_rows <= 1024) on the GPU:
+   path [2][n_rows + n_cols], *path_len valid entries of each */
+int wh_dtw(wh_ctx* ctx, const float* x, int n_rows, int n_cols, int* path, int* path_len);
+
 /* cumulative stage wall times in ms: [0] mel [1] encode [2] prefill [3] steps
    [4] step count [5] encode windows */
 int wh_stats(wh_ctx* ctx, double* out, int n);

@@ -200,6 +200,62 @@ def transcribe_goldens(model, name: str, out: dict):
         json.dump(dict(audio_seconds=65.0, audio_seed=7, runs=runs, segments=segs_all), f, indent=0)
 
 
+def words_goldens(model, name: str):
+    """Word-level timestamps (config 5 / SURVEY §8 a19): the reference's own
+    find_alignment on one window, and transcribe(word_timestamps=True) on 65 s of
+    audio; plus the decoded bytes of every token id involved (the product ships no
+    BPE rank file, so tests install these few ids with tokenizer.set_token_bytes)."""
+    import base64
+    dims = syn.MODEL_DIMS[name]
+    tok = ref_tok.get_tokenizer(dims["n_vocab"] >= 51865, num_languages=dims["n_vocab"] - 51765 -
+                                int(dims["n_vocab"] >= 51865), language="en", task="transcribe")
+    audio = syn.synthetic_audio(65.0, seed=7)
+    ids = set()
+    res = {"audio_seconds": 65.0, "audio_seed": 7, "runs": {}, "segments": {}, "find_alignment": {}}
+    # direct find_alignment on window 0 with a fixed text
+    mel = ref_audio.log_mel_spectrogram(audio, dims["n_mels"], padding=N_SAMPLES)
+    seg = ref_audio.pad_or_trim(mel[:, :3000], 3000)
+    with torch.no_grad():
+        model.decoder.cross_k_caches, model.decoder.cross_v_caches = model.decoder.crossKVCaches(
+            model.encoder(seg.unsqueeze(0)))
+        model.text_offset = 0
+    rng = np.random.default_rng(5)
+    for key, ntok, nf in [("a", 17, 3000), ("b", 40, 2200), ("c", 3, 800)]:
+        text = [int(t) for t in rng.integers(0, tok.eot, ntok)]
+        ids.update(text)
+        al = ref_timing.find_alignment(model, tok, text, nf)
+        res["find_alignment"][key] = dict(
+            text_tokens=text, num_frames=nf,
+            words=[dict(word=w.word, tokens=[int(t) for t in w.tokens], start=float(w.start), end=float(w.end),
+                        probability=float(w.probability)) for w in al])
+    runs = {
+        "seq_greedy_words": dict(condition_on_previous_text=True, word_timestamps=True),
+        "clip_beam_words": dict(beam_size=5, condition_on_previous_text=False, clip_timestamps="0,30,30,60,60",
+                                word_timestamps=True),
+        "clip_greedy_words": dict(condition_on_previous_text=False, clip_timestamps="0,30,30,60,60",
+                                  word_timestamps=True),
+        "seq_greedy_halluc": dict(condition_on_previous_text=True, word_timestamps=True,
+                                  hallucination_silence_threshold=2.0),
+    }
+    for key, kw in runs.items():
+        t0 = time.time()
+        out = refw.transcribe(model, audio, temperature=0.0, language="en", fp16=False, verbose=None, **kw)
+        segs = []
+        for s_ in out["segments"]:
+            ids.update(int(t) for t in s_["tokens"])
+            segs.append(dict(seek=s_["seek"], start=s_["start"], end=s_["end"], tokens=[int(t) for t in s_["tokens"]],
+                             words=[dict(word=w["word"], start=w["start"], end=w["end"],
+                                         probability=float(w["probability"])) for w in s_.get("words", [])]))
+        res["runs"][key] = kw
+        res["segments"][key] = segs
+        print(f"[{name}] transcribe {key}: {len(segs)} segs {time.time()-t0:.1f}s", flush=True)
+    dec = tok.encoding._decoder
+    res["token_bytes"] = {str(i): base64.b64encode(dec[i]).decode() for i in sorted(ids) if i < tok.eot}
+    res["encoding"] = tok.encoding.name
+    with open(os.path.join(OUT, f"{name}_words.json"), "w") as f:
+        json.dump(res, f, indent=0)
+
+
 def mel_goldens():
     out = {}
     out["filters_80"] = ref_audio.mel_filters("cpu", 80).numpy()
@@ -338,6 +394,9 @@ def main(argv):
             dtw_goldens()
         elif w == "assets":
             asset_export()
+        elif w.endswith("_words"):
+            model, _ = build_ref_model(w[:-len("_words")])
+            words_goldens(model, w[:-len("_words")])
         else:
             small = w.startswith("micro")
             big = w in ("turbo", "large-v3", "large-v3-turbo")

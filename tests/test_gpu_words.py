@@ -1,0 +1,140 @@
+"""Word-level timestamps (config 5) on the GPU: wh_dtw / wh_align
+(csrc/wh_align.hip) against the reference's own outputs and the CPU oracle.
+
+* DTW: bit-exact paths against dtw.npz (the reference's dtw_cpu on planted-path
+  and random matrices, up to 123 x 1500) and against oracle/ref_timing on edge
+  shapes and all-tie matrices.
+* find_alignment: the device half (matrix + path + token probabilities) against
+  the oracle on the same audio features; the whole function and transcribe(...,
+  word_timestamps=True) against the reference (micro_words.json) in fp32.
+Tolerances: paths and word boundaries exact; token probabilities rel 1e-3
+(fp32 softmax of logits that agree to ~1e-5 with the reference's)."""
+import base64
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import GOLDEN
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def words_golden():
+    with open(os.path.join(GOLDEN, "micro_words.json")) as f:
+        return json.load(f)
+
+
+@pytest.fixture(scope="module")
+def micro32(words_golden):
+    import whisper
+    from whisper import tokenizer as T
+    enc = words_golden["encoding"].replace(".tiktoken", "")
+    T.set_token_bytes(enc, {int(k): base64.b64decode(v) for k, v in words_golden["token_bytes"].items()})
+    m = whisper.load_model("micro", device=0, dtype="fp32", max_windows=4, max_group=5)
+    yield m
+    m.close()
+    T.set_token_bytes(enc, None)
+
+
+def test_gpu_dtw_matches_reference(micro32):
+    g = np.load(os.path.join(GOLDEN, "dtw.npz"))
+    n = 0
+    for key in g.files:
+        if key.endswith("_x") and (key.startswith("planted_") or key.startswith("rand_")):
+            base = key[:-2]
+            want = g[base + "_trace"] if key.startswith("planted_") else g[base + "_path"]
+            got = micro32.ctx.dtw(g[key])
+            np.testing.assert_array_equal(got, want, err_msg=key)
+            n += 1
+    assert n == 7
+
+
+@pytest.mark.parametrize("shape", [(1, 1), (1, 9), (9, 1), (3, 3), (17, 5), (5, 300)])
+@pytest.mark.parametrize("kind", ["zeros", "ints", "randn"])
+def test_gpu_dtw_edges_and_ties(micro32, shape, kind):
+    """all-equal and small-integer costs make every comparison a tie: the
+    if/elif/else order must match dtw_cpu exactly."""
+    from oracle import ref_timing as RT
+    rng = np.random.default_rng(hash((shape, kind)) % 2**32)
+    x = {"zeros": np.zeros(shape), "ints": rng.integers(0, 3, shape).astype(np.float64),
+         "randn": rng.standard_normal(shape)}[kind].astype(np.float32)
+    np.testing.assert_array_equal(micro32.ctx.dtw(x), RT.dtw_cpu(x.astype(np.float64)))
+
+
+def _window0(m, gw):
+    import whisper
+    from whisper import synthetic as S
+    audio = S.synthetic_audio(gw["audio_seconds"], seed=gw["audio_seed"])
+    mel = whisper.log_mel_spectrogram(audio, m.dims.n_mels, padding=whisper.audio.N_SAMPLES)
+    seg = whisper.pad_or_trim(mel[:, :3000], 3000)
+    m.ctx.mel_write(seg)
+    m.ctx.encode([0], [3000])
+    m._last_windows = ([0], [3000])
+
+
+def test_align_device_half_matches_oracle(micro32, words_golden):
+    """wh_align vs oracle/ref_timing.find_alignment_path on the same audio features."""
+    from oracle import ref_timing as RT
+    from oracle import ref_whisper as R
+    from whisper import synthetic as S
+    from whisper.timing import _alignment_head_ids
+    m = micro32
+    _window0(m, words_golden)
+    xa = m.ctx.audio_features(0)
+    dims = S.MODEL_DIMS["micro"]
+    om = R.OracleWhisper(dims, S.synthetic_state_dict(dims, 0))
+    om.set_audio(torch.from_numpy(xa))
+    st = R.SpecialTokens.for_model(dims)
+    tok_nots = st.no_timestamps
+    for key, case in words_golden["find_alignment"].items():
+        text, nf = case["text_tokens"], case["num_frames"]
+        probs, ti, tm = m.ctx.align(0, [*st.sot_sequence, tok_nots, *text, st.eot], len(st.sot_sequence), nf,
+                                    _alignment_head_ids(m))
+        rp, rti, rtm, _ = RT.find_alignment_path(om, st.sot_sequence, tok_nots, st.eot, text, nf)
+        np.testing.assert_allclose(probs, rp, rtol=1e-3, err_msg=key)
+        np.testing.assert_array_equal(ti, rti, err_msg=key)
+        np.testing.assert_array_equal(tm, rtm, err_msg=key)
+
+
+def test_find_alignment_matches_reference(micro32, words_golden):
+    from whisper.tokenizer import get_tokenizer
+    from whisper.timing import find_alignment
+    m = micro32
+    _window0(m, words_golden)
+    tok = get_tokenizer(m.is_multilingual, num_languages=m.num_languages, language="en", task="transcribe")
+    for key, case in words_golden["find_alignment"].items():
+        got = find_alignment(m, tok, case["text_tokens"], case["num_frames"])
+        ref = case["words"]
+        assert [w.word for w in got] == [w["word"] for w in ref], key
+        assert [w.tokens for w in got] == [w["tokens"] for w in ref], key
+        np.testing.assert_allclose([w.start for w in got], [w["start"] for w in ref], rtol=0, atol=1e-9)
+        np.testing.assert_allclose([w.end for w in got], [w["end"] for w in ref], rtol=0, atol=1e-9)
+        np.testing.assert_allclose([w.probability for w in got], [w["probability"] for w in ref], rtol=1e-3)
+
+
+@pytest.mark.parametrize("run,schedule", [("seq_greedy_words", "auto"), ("clip_greedy_words", "auto"),
+                                          ("clip_beam_words", "auto"), ("clip_greedy_words", "sequential"),
+                                          ("seq_greedy_halluc", "auto")])
+def test_transcribe_word_timestamps(micro32, words_golden, run, schedule):
+    """transcribe(word_timestamps=True) equals the reference's segments and words;
+    clip runs under "auto" take the batched schedule (alignment per window in the
+    round, words re-derived in clip order)."""
+    import whisper
+    from whisper import synthetic as S
+    m = micro32
+    kw = dict(words_golden["runs"][run])
+    audio = S.synthetic_audio(words_golden["audio_seconds"], seed=words_golden["audio_seed"])
+    out = whisper.transcribe(m, audio, temperature=0.0, language="en", schedule=schedule, **kw)
+    ref = words_golden["segments"][run]
+    assert [s["tokens"] for s in out["segments"]] == [s["tokens"] for s in ref]
+    assert [s["seek"] for s in out["segments"]] == [s["seek"] for s in ref]
+    for a, b in zip(out["segments"], ref):
+        assert a["start"] == pytest.approx(b["start"]) and a["end"] == pytest.approx(b["end"])
+        assert [w["word"] for w in a["words"]] == [w["word"] for w in b["words"]]
+        for wa, wb in zip(a["words"], b["words"]):
+            assert wa["start"] == pytest.approx(wb["start"]) and wa["end"] == pytest.approx(wb["end"])
+            assert wa["probability"] == pytest.approx(wb["probability"], rel=1e-3)

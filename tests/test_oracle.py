@@ -86,3 +86,57 @@ def test_micro_transcribe(micro, run):
     for a, b in zip(segs, ref):
         assert a["start"] == pytest.approx(b["start"]) and a["end"] == pytest.approx(b["end"])
         assert a["avg_logprob"] == pytest.approx(b["avg_logprob"], abs=1e-4)
+
+
+# ----------------------------------------------------------------------------- timing.py
+def test_dtw_oracle_against_reference():
+    """oracle/ref_timing.dtw_cpu vs the reference's dtw_cpu outputs (dtw.npz): planted
+    paths (the construction of the reference's tests/test_timing.py) and random paths."""
+    from oracle import ref_timing as RT
+    g = _golden("dtw")
+    for key in g.files:
+        if key.startswith("planted_") and key.endswith("_x"):
+            base = key[:-2]
+            if base == "planted_123x1500":
+                continue  # 184k cells in numpy: covered on the GPU (tests/test_gpu_words.py)
+            np.testing.assert_array_equal(RT.dtw_cpu(g[key].astype(np.float64)), g[base + "_trace"])
+        if key.startswith("rand_") and key.endswith("_x"):
+            base = key[:-2]
+            np.testing.assert_array_equal(RT.dtw_cpu(g[key].astype(np.float64)), g[base + "_path"])
+
+
+def test_median_filter_oracle_against_reference():
+    from oracle import ref_timing as RT
+    g = _golden("dtw")
+    for key in g.files:
+        if key.startswith("med_") and key.endswith("_x"):
+            base = key[:-2]
+            x = torch.from_numpy(g[key])
+            for w in (3, 5, 7, 13):
+                np.testing.assert_array_equal(RT.median_filter(x, w).numpy(), g[f"{base}_w{w}"])
+
+
+def test_word_split_matches_reference_alignment_words():
+    """Product tokenizer word splitting (tokenizer.py:277-327 restated) reproduces the
+    words/token groups of the reference's find_alignment (micro_words.json)."""
+    import base64
+    from whisper import tokenizer as T
+    with open(os.path.join(GOLDEN, "micro_words.json")) as f:
+        gw = json.load(f)
+    enc = gw["encoding"].replace(".tiktoken", "")
+    T.set_token_bytes(enc, {int(k): base64.b64decode(v) for k, v in gw["token_bytes"].items()})
+    try:
+        tok = T.get_tokenizer(True, num_languages=S.MODEL_DIMS["micro"]["n_vocab"] - 51765 - 1, language="en",
+                              task="transcribe")
+        for case in gw["find_alignment"].values():
+            words, word_tokens = tok.split_to_word_tokens(case["text_tokens"] + [tok.eot])
+            ref = case["words"]
+            if len(word_tokens) <= 1:
+                assert ref == []
+                continue
+            # find_alignment zips words with len(word_tokens) - 1 boundaries: the eot word drops
+            assert len(ref) == len(words) - 1
+            assert [w["word"] for w in ref] == words[:-1]
+            assert [w["tokens"] for w in ref] == word_tokens[:-1]
+    finally:
+        T.set_token_bytes(enc, None)

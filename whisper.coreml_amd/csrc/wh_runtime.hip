@@ -18,6 +18,7 @@
 #include <chrono>
 
 #include "whisper_hip.h"
+#include "wh_align.h"
 #include "wh_gemm.h"
 #include "wh_kernels.h"
 
@@ -107,6 +108,9 @@ struct wh_ctx {
   virtual int decode_read(int slot, int* tokens, float* slp, int* len, int* fin_n, int* fin_tok, int* fin_len,
                           float* fin_score, float* nsp) = 0;
   virtual int prefill_logits(int slot, const int* tokens, int n, float* logits, const int* ah, int na, float* aqk) = 0;
+  virtual int align(int slot, const int* tokens, int n, int n_sot, int num_frames, const int* ah, int na, int medfilt,
+                    float* probs, int* path, int* plen) = 0;
+  virtual int dtw(const float* x, int N, int M, int* path, int* plen) = 0;
   virtual int time_stage(int what, int iters, double* ms) = 0;
   std::vector<float> token_ms;  // per-token wall ms of each decode_steps chunk
   double stats[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -986,33 +990,127 @@ struct Ctx : public wh_ctx {
   // Whisper.forward (model.py:110-119): all-row logits of a first pass for one window,
   // optional raw cross-QK of alignment heads.  Uses beam slot 0 of `slot` and the anc
   // table with a 1-beam layout; call it when no decode of that slot is in flight.
-  int prefill_logits(int slot, const int* tokens, int n, float* lg, const int* ah, int na, float* aqk) override {
+  // first pass of `n` tokens at offset 0 for one window slot (beam slot 0, a 1-beam
+  // anc layout), optional raw cross-QK of the alignment heads into d_aqk [na][n][1500];
+  // on return xn_d holds the final LayerNorm of every row.  The host vectors are kept
+  // alive in `keep` until the caller synchronises.
+  int first_pass(int slot, const int* tokens, int n, const int* ah, int na, float* d_aqk,
+                 std::vector<std::vector<int>>& keep) {
     if (!finalized) return fail(-9, "weights not finalized");
     if (slot < 0 || slot >= Wcap || n < 1 || n > CTX) return fail(-15, "bad slot or token count");
     for (int i = 0; i < n; ++i)
       if (tokens[i] < 0 || tokens[i] >= V) return fail(-15, "token out of vocabulary");
-    std::vector<int> rt(tokens, tokens + n), rp(n), rw(n, slot), rs(n, 0), one0{0}, onen{n}, onesl{slot};
+    keep.assign(9, {});
+    auto& rt = keep[0]; auto& rp = keep[1]; auto& rw = keep[2]; auto& rs = keep[3];
+    rt.assign(tokens, tokens + n); rp.resize(n); rw.assign(n, slot); rs.assign(n, 0);
+    keep[4] = {0}; keep[5] = {n}; keep[6] = {slot};
     for (int i = 0; i < n; ++i) rp[i] = i;
-    std::vector<int> anc0((size_t)CTX, 0);
-    std::vector<int> map((size_t)Ld * nh, -1);
+    keep[7].assign((size_t)CTX, 0);
+    auto& map = keep[8];
+    map.assign((size_t)Ld * nh, -1);
     for (int i = 0; i < na; ++i)
       if (ah[i] >= 0 && ah[i] < Ld * nh) map[ah[i]] = i;
     HIPCHK(hipMemcpyAsync(row_tok, rt.data(), n * 4, hipMemcpyHostToDevice, st));
     HIPCHK(hipMemcpyAsync(row_pos, rp.data(), n * 4, hipMemcpyHostToDevice, st));
     HIPCHK(hipMemcpyAsync(row_win, rw.data(), n * 4, hipMemcpyHostToDevice, st));
     HIPCHK(hipMemcpyAsync(row_slot, rs.data(), n * 4, hipMemcpyHostToDevice, st));
-    HIPCHK(hipMemcpyAsync(win_row0, one0.data(), 4, hipMemcpyHostToDevice, st));
-    HIPCHK(hipMemcpyAsync(win_nrows, onen.data(), 4, hipMemcpyHostToDevice, st));
-    HIPCHK(hipMemcpyAsync(win_slot, onesl.data(), 4, hipMemcpyHostToDevice, st));
-    HIPCHK(hipMemcpyAsync(S.anc + (size_t)slot * CTX, anc0.data(), CTX * 4, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(win_row0, keep[4].data(), 4, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(win_nrows, keep[5].data(), 4, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(win_slot, keep[6].data(), 4, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(S.anc + (size_t)slot * CTX, keep[7].data(), CTX * 4, hipMemcpyHostToDevice, st));
     HIPCHK(hipMemcpyAsync(qk_map, map.data(), map.size() * 4, hipMemcpyHostToDevice, st));
+    launch_embed<T>(E, Pdec, ns, row_tok, row_pos, nullptr, nullptr, 1, HCTX, CTX - 1, x_d, n, st);
+    return dec_layers(n, row_win, row_slot, row_pos, 1, 1, win_row0, win_nrows, win_slot, d_aqk,
+                      d_aqk ? qk_map : nullptr, n);
+  }
+
+  // grow-only device scratch for the alignment / prefill readbacks
+  char* scratch = nullptr;
+  size_t scratch_cap = 0;
+  int ensure_scratch(size_t bytes) {
+    if (bytes <= scratch_cap) return 0;
+    HIPCHK(hipStreamSynchronize(st));
+    if (scratch) hipFree(scratch);
+    scratch = nullptr;
+    scratch_cap = 0;
+    HIPCHK(hipMalloc((void**)&scratch, bytes));
+    scratch_cap = bytes;
+    return 0;
+  }
+
+  // find_alignment's device half (timing.py:163-231): first pass over
+  // sot_sequence + [no_timestamps] + text + [eot] with the alignment heads' cross-QK,
+  // the text tokens' probabilities, the filtered head-mean matrix and its DTW path.
+  int align(int slot, const int* tokens, int n, int n_sot, int num_frames, const int* ah, int na, int medfilt,
+            float* probs, int* path, int* plen) override {
+    const int Tt = n - n_sot - 2, N = n - n_sot - 1, F = num_frames / 2;
+    if (n_sot < 1 || Tt < 1) return fail(-15, "align: need sot_sequence + no_timestamps + >= 1 text token + eot");
+    if (F < 1 || F > 1500) return fail(-15, "align: num_frames out of range");
+    if (na < 1 || na > Ld * nh) return fail(-15, "align: alignment head count");
+    if (medfilt < 1 || medfilt > 15 || medfilt % 2 == 0) return fail(-15, "align: medfilt_width must be odd <= 15");
+    const size_t b_qk = (size_t)na * n * 1500 * 4, b_lg = (size_t)std::min(Tt, 128) * V * 4,
+                 b_mat = (size_t)N * F * 4, b_tr = (size_t)(N + 1) * (F + 1), b_path = (size_t)2 * (N + F) * 4;
+    auto al = [](size_t b) { return (b + 255) & ~size_t(255); };
+    TRY(ensure_scratch(al(b_qk) + al(b_lg) + al(b_mat) + al(b_tr) + al(b_path) + 3 * al((size_t)Tt * 4 + 16)));
+    char* p = scratch;
+    float* d_qk = (float*)p; p += al(b_qk);
+    float* d_lg = (float*)p; p += al(b_lg);
+    float* d_mat = (float*)p; p += al(b_mat);
+    signed char* d_tr = (signed char*)p; p += al(b_tr);
+    int* d_path = (int*)p; p += al(b_path);
+    float* d_probs = (float*)p; p += al((size_t)Tt * 4 + 16);
+    int* d_tok = (int*)p; p += al((size_t)Tt * 4 + 16);
+    int* d_plen = (int*)p;
+    std::vector<std::vector<int>> keep;
+    TRY(first_pass(slot, tokens, n, ah, na, d_qk, keep));
+    // logits of the rows that predict the text tokens, 128 rows at a time
+    std::vector<int> sel(Tt);
+    for (int k = 0; k < Tt; ++k) sel[k] = n_sot + k;
+    HIPCHK(hipMemcpyAsync(d_tok, tokens + n_sot + 1, Tt * 4, hipMemcpyHostToDevice, st));
+    for (int r0 = 0; r0 < Tt; r0 += 128) {
+      const int rr = std::min(128, Tt - r0);
+      HIPCHK(hipMemcpyAsync(rows_in, sel.data() + r0, rr * 4, hipMemcpyHostToDevice, st));
+      TRY(vocab(rows_in, rr, d_lg));
+      launch_token_probs(d_lg, V, 0, rr, tokens[n - 1], d_tok + r0, d_probs + r0, st);
+      HIPCHK(hipStreamSynchronize(st));  // rows_in / d_lg are reused by the next chunk
+    }
+    launch_align_matrix(d_qk, n, 1500, F, na, n_sot, N, medfilt, d_mat, st);
+    if (launch_dtw(d_mat, N, F, -1.f, d_tr, d_path, d_plen, st)) return fail(-15, "align: too many token rows");
+    HIPCHK(hipMemcpyAsync(probs, d_probs, Tt * 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(plen, d_plen, 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(path, d_path, b_path, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    HIPCHK(hipGetLastError());
+    return 0;
+  }
+
+  // timing.dtw (timing.py:82-105, 139-151) of a host cost matrix x [N][M] on the GPU
+  int dtw(const float* x, int N, int M, int* path, int* plen) override {
+    if (N < 1 || M < 1 || N > 1024 || (int64_t)N * M > (int64_t)1 << 26) return fail(-15, "dtw: shape out of range");
+    auto al = [](size_t b) { return (b + 255) & ~size_t(255); };
+    const size_t b_x = (size_t)N * M * 4, b_tr = (size_t)(N + 1) * (M + 1), b_path = (size_t)2 * (N + M) * 4;
+    TRY(ensure_scratch(al(b_x) + al(b_tr) + al(b_path) + 256));
+    char* p = scratch;
+    float* d_x = (float*)p; p += al(b_x);
+    signed char* d_tr = (signed char*)p; p += al(b_tr);
+    int* d_path = (int*)p; p += al(b_path);
+    int* d_plen = (int*)p;
+    HIPCHK(hipMemcpyAsync(d_x, x, b_x, hipMemcpyHostToDevice, st));
+    TRY(launch_dtw(d_x, N, M, 1.f, d_tr, d_path, d_plen, st) ? fail(-15, "dtw launch") : 0);
+    HIPCHK(hipMemcpyAsync(plen, d_plen, 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(path, d_path, b_path, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    HIPCHK(hipGetLastError());
+    return 0;
+  }
+
+  int prefill_logits(int slot, const int* tokens, int n, float* lg, const int* ah, int na, float* aqk) override {
     float* d_aqk = nullptr;
     float* out = nullptr;
     if (na > 0 && aqk) HIPCHK(hipMalloc((void**)&d_aqk, (size_t)na * n * 1500 * 4));
     HIPCHK(hipMalloc((void**)&out, (size_t)n * V * 4));
-    launch_embed<T>(E, Pdec, ns, row_tok, row_pos, nullptr, nullptr, 1, HCTX, CTX - 1, x_d, n, st);
-    int rc = dec_layers(n, row_win, row_slot, row_pos, 1, 1, win_row0, win_nrows, win_slot, d_aqk,
-                        d_aqk ? qk_map : nullptr, n);
+    std::vector<std::vector<int>> keep;
+    int rc = first_pass(slot, tokens, n, ah, na, d_aqk, keep);
     std::vector<int> s2(n);
     for (int i = 0; i < n; ++i) s2[i] = i;
     for (int r0 = 0; r0 < n && rc == 0; r0 += 128) {
@@ -1198,6 +1296,14 @@ int wh_decode_read(wh_ctx* ctx, int slot, int* tokens, float* slp, int* len, int
 int wh_decode_maxc(wh_ctx* ctx) { return ctx ? ctx->maxc_stride : -1; }
 int wh_prefill_logits(wh_ctx* ctx, int slot, const int* tokens, int n, float* logits, const int* ah, int na, float* aqk) {
   CTXCALL(ctx->prefill_logits(slot, tokens, n, logits, ah, na, aqk));
+}
+int wh_align(wh_ctx* ctx, int slot, const int* tokens, int n_tokens, int n_sot, int num_frames, const int* align_heads,
+             int n_align, int medfilt_width, float* token_probs, int* path, int* path_len) {
+  CTXCALL(ctx->align(slot, tokens, n_tokens, n_sot, num_frames, align_heads, n_align, medfilt_width, token_probs, path,
+                     path_len));
+}
+int wh_dtw(wh_ctx* ctx, const float* x, int n_rows, int n_cols, int* path, int* path_len) {
+  CTXCALL(ctx->dtw(x, n_rows, n_cols, path, path_len));
 }
 int wh_stats(wh_ctx* ctx, double* out, int n) {
   if (!ctx || !out) return fail(-1, "null argument");

@@ -67,6 +67,9 @@ _EXPORTS = {
                                c_void_p, c_void_p]),
     "wh_decode_maxc": (c_int, [c_void_p]),
     "wh_prefill_logits": (c_int, [c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p]),
+    "wh_align": (c_int, [c_void_p, c_int, c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_int, c_void_p, c_void_p,
+                         POINTER(c_int)]),
+    "wh_dtw": (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p, POINTER(c_int)]),
     "wh_stats": (c_int, [c_void_p, POINTER(c_double), c_int]),
     "wh_sync": (c_int, [c_void_p]),
     "wh_time_stage": (c_int, [c_void_p, c_int, c_int, POINTER(c_double)]),
@@ -266,6 +269,30 @@ class HipContext:
                                                _ptr(ah) if len(ah) else None, len(ah),
                                                _ptr(qk) if qk is not None else None), "wh_prefill_logits")
         return lg, qk
+
+    def align(self, slot: int, tokens: Sequence[int], n_sot: int, num_frames: int, align_heads: Sequence[int],
+              medfilt_width: int = 7):
+        """find_alignment's device half (timing.py:163-231): returns (text_token_probs [T],
+        text_indices, time_indices) of dtw(-matrix)."""
+        t = np.ascontiguousarray(tokens, dtype=np.int32)
+        ah = np.ascontiguousarray(align_heads, dtype=np.int32)
+        T = len(t) - n_sot - 2
+        probs = np.zeros(max(T, 1), dtype=np.float32)
+        width = (T + 1) + num_frames // 2
+        path = np.zeros((2, width), dtype=np.int32)
+        n = c_int(0)
+        self._check(self.lib.wh_align(self.h, slot, _ptr(t), len(t), n_sot, num_frames, _ptr(ah), len(ah),
+                                      medfilt_width, _ptr(probs), _ptr(path), ctypes.byref(n)), "wh_align")
+        return probs[:T], path[0, :n.value].copy(), path[1, :n.value].copy()
+
+    def dtw(self, x: np.ndarray) -> np.ndarray:
+        """timing.dtw(x) on the GPU: [2][path length] (text indices, time indices)."""
+        x = np.ascontiguousarray(x, dtype=np.float32)
+        N, M = x.shape
+        path = np.zeros((2, N + M), dtype=np.int32)
+        n = c_int(0)
+        self._check(self.lib.wh_dtw(self.h, _ptr(x), N, M, _ptr(path), ctypes.byref(n)), "wh_dtw")
+        return path[:, :n.value].copy()
 
     def stats(self) -> dict:
         out = (c_double * 8)()

@@ -12,6 +12,7 @@ directory holding it to enable ``decode``; without it ``decode`` returns "".
 import base64
 import json
 import os
+import string
 from dataclasses import dataclass, field
 from functools import lru_cache
 from typing import Dict, List, Optional, Tuple
@@ -29,8 +30,26 @@ LANGUAGES: Dict[str, str] = {c: n for c, n in _specials()["languages"]}
 TO_LANGUAGE_CODE: Dict[str, str] = {**{n: c for c, n in LANGUAGES.items()}, **_specials()["to_language_code"]}
 
 
-@lru_cache(maxsize=None)
+_RANK_OVERRIDE: Dict[str, Dict[int, bytes]] = {}
+
+
+def set_token_bytes(encoding_name: str, table: Optional[Dict[int, bytes]]):
+    """Install (or with None remove) an id -> bytes table for `encoding_name` in place
+    of the BPE rank file (tests ship the few ids their fixtures decode)."""
+    if table is None:
+        _RANK_OVERRIDE.pop(encoding_name, None)
+    else:
+        _RANK_OVERRIDE[encoding_name] = dict(table)
+
+
 def _ranks(name: str) -> Optional[Dict[int, bytes]]:
+    if name in _RANK_OVERRIDE:
+        return _RANK_OVERRIDE[name]
+    return _rank_file(name)
+
+
+@lru_cache(maxsize=None)
+def _rank_file(name: str) -> Optional[Dict[int, bytes]]:
     d = os.environ.get("WHISPER_TIKTOKEN_DIR")
     if not d:
         return None
@@ -159,6 +178,55 @@ class Tokenizer:
         for t in token_ids:
             out += ranks[t] if t in ranks else inv.get(t, "").encode()
         return out.decode("utf-8", errors="replace")
+
+    # word splitting for word-level timestamps (tokenizer.py:277-327)
+    def split_to_word_tokens(self, tokens: List[int]):
+        if _ranks(self.encoding_name) is None:
+            raise RuntimeError("word timestamps need the BPE rank file: set WHISPER_TIKTOKEN_DIR "
+                               f"to a directory holding {self.encoding_name}.tiktoken")
+        if self.language in {"zh", "ja", "th", "lo", "my", "yue"}:
+            return self.split_tokens_on_unicode(tokens)
+        return self.split_tokens_on_spaces(tokens)
+
+    def split_tokens_on_unicode(self, tokens: List[int]):
+        decoded_full = self.decode_with_timestamps(tokens)
+        replacement_char = "\ufffd"
+
+        words = []
+        word_tokens = []
+        current_tokens = []
+        unicode_offset = 0
+
+        for token in tokens:
+            current_tokens.append(token)
+            decoded = self.decode_with_timestamps(current_tokens)
+
+            if (replacement_char not in decoded
+                    or decoded_full[unicode_offset + decoded.index(replacement_char)] == replacement_char):
+                words.append(decoded)
+                word_tokens.append(current_tokens)
+                current_tokens = []
+                unicode_offset += len(decoded)
+
+        return words, word_tokens
+
+    def split_tokens_on_spaces(self, tokens: List[int]):
+        subwords, subword_tokens_list = self.split_tokens_on_unicode(tokens)
+        words = []
+        word_tokens = []
+
+        for subword, subword_tokens in zip(subwords, subword_tokens_list):
+            special = subword_tokens[0] >= self.eot
+            with_space = subword.startswith(" ")
+            punctuation = subword.strip() in string.punctuation
+            if special or with_space or punctuation or len(words) == 0:
+                words.append(subword)
+                word_tokens.append(subword_tokens)
+            else:
+                words[-1] = words[-1] + subword
+                word_tokens[-1].extend(subword_tokens)
+
+        return words, word_tokens
 
 
 @lru_cache(maxsize=None)

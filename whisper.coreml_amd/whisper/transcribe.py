@@ -6,19 +6,25 @@ empty-segment clearing).  Two schedules:
 
 * sequential — the reference order, one window at a time; required whenever a
   window depends on the previous one (``condition_on_previous_text=True``,
-  ``carry_initial_prompt``, word timestamps);
+  ``carry_initial_prompt``, ``hallucination_silence_threshold``);
 * batched — with ``condition_on_previous_text=False`` and several clips
   (``clip_timestamps`` on a grid), windows of different clips are independent
   (each clip's seek is clip-local, the prompt resets every window:
   transcribe.py:277-287, 513-515), so every round encodes and decodes the next
   window of *all* unfinished clips together on the GPU.  Segments are assembled
   in clip order afterwards, which reproduces the reference's output exactly.
+  With word timestamps the alignment of every window runs in the round (GPU);
+  the words are then re-derived in clip order with the reference's running
+  ``last_speech_timestamp``; if that would move any window's seek (it can only
+  through a one-word last segment) the file is re-run sequentially.
 
 The log-mel of the whole file is computed on the GPU and stays there; windows
 are cut from it on the device.
 """
 
+import copy
 import os
+import warnings
 from dataclasses import replace
 from typing import TYPE_CHECKING, List, Optional, Tuple, Union
 
@@ -27,6 +33,7 @@ import numpy as np
 from .audio import FRAMES_PER_SECOND, HOP_LENGTH, N_FRAMES, N_SAMPLES, SAMPLE_RATE, load_audio
 from .backend_hip import DeviceAudio
 from .decoding import DecodingOptions, DecodingResult, detect_language, run_windows
+from .timing import apply_alignment, find_alignment
 from .tokenizer import LANGUAGES, get_tokenizer
 
 if TYPE_CHECKING:
@@ -72,8 +79,10 @@ def _decode_with_fallback(model, base_opts: DecodingOptions, temperatures, promp
 
 
 def _split_segments(tokenizer, result: DecodingResult, seek: int, time_offset: float, segment_size: int,
-                    segment_duration: float, input_stride: int, time_precision: float) -> Tuple[List[dict], int]:
-    """Segment building and seek advance of transcribe.py:350-410."""
+                    segment_duration: float, input_stride: int, time_precision: float
+                    ) -> Tuple[List[dict], int, bool]:
+    """Segment building and seek advance of transcribe.py:350-410; returns (segments,
+    seek, single_timestamp_ending)."""
     tokens = np.asarray(result.tokens, dtype=np.int64)
     tb = tokenizer.timestamp_begin
 
@@ -108,12 +117,16 @@ def _split_segments(tokenizer, result: DecodingResult, seek: int, time_offset: f
             duration = (int(ts[-1]) - tb) * time_precision
         segs.append(new_segment(time_offset, time_offset + duration, tokens))
         seek += segment_size
-    for s in segs:  # transcribe.py:494-499
+    return segs, seek, single_end
+
+
+def _clear_empty(tokenizer, segs: List[dict]):
+    """transcribe.py:494-499 (after word timestamps)."""
+    for s in segs:
         if s["start"] == s["end"] or tokenizer.is_blank_text(s["tokens"]):
             s["text"] = ""
             s["tokens"] = []
             s["words"] = []
-    return segs, seek
 
 
 def transcribe(model: "Whisper", audio: Union[str, np.ndarray], *, verbose: Optional[bool] = None,
@@ -130,8 +143,6 @@ def transcribe(model: "Whisper", audio: Union[str, np.ndarray], *, verbose: Opti
     "batched") and ``mel_max_reduce`` (callable local max -> global max, used when
     one file is sharded over GPUs: the log-mel floor is a whole-file max,
     audio.py:155, so ranks all-reduce it before normalizing)."""
-    if word_timestamps:
-        raise NotImplementedError("word_timestamps on the HIP backend is planned (SURVEY §8(f) rank 1)")
     if decode_options.get("fp16", True) is False and model.dtype != "fp32":
         pass  # the compute precision is fixed when the model is loaded (dtype=...)
     decode_options.pop("fp16", None)
@@ -209,14 +220,21 @@ def transcribe(model: "Whisper", audio: Union[str, np.ndarray], *, verbose: Opti
         raise NotImplementedError("text initial_prompt needs a BPE encoder; pass a list of token ids")
     initial_prompt_tokens = list(initial_prompt) if initial_prompt else []
 
+    if word_timestamps and task == "translate":
+        warnings.warn("Word-level timestamps on translations may not be reliable.")
     batched = schedule == "batched" or (
         schedule == "auto" and not condition_on_previous_text and not carry_initial_prompt
         and not initial_prompt_tokens and len(seek_clips) > 1)
-    state = dict(content_frames=content_frames, tokenizer=tokenizer, temperatures=temperatures,
-                 thresholds=thresholds, base=base, input_stride=input_stride, time_precision=time_precision)
+    if hallucination_silence_threshold is not None and word_timestamps:
+        batched = False  # its seek rules read the running last_speech_timestamp
+    state = dict(content_frames=content_frames, content_duration=content_duration, tokenizer=tokenizer,
+                 temperatures=temperatures, thresholds=thresholds, base=base, input_stride=input_stride,
+                 time_precision=time_precision, word_timestamps=word_timestamps, prepend=prepend_punctuations,
+                 append=append_punctuations, hallucination=hallucination_silence_threshold)
+    segments = None
     if batched:
         segments = _run_batched(model, seek_clips, initial_prompt_tokens, state)
-    else:
+    if segments is None:
         segments = _run_sequential(model, seek_clips, initial_prompt_tokens, condition_on_previous_text,
                                    carry_initial_prompt, state)
     all_tokens = list(initial_prompt_tokens)
@@ -235,21 +253,78 @@ def _window_at(seek: int, clip: Tuple[int, int], content_frames: int):
     return segment_size, segment_size * HOP_LENGTH / SAMPLE_RATE
 
 
-def _apply_result(model, result, seek, segment_size, st) -> Tuple[List[dict], int, bool]:
+def _apply_result(model, result, seek, segment_size, st) -> Tuple[List[dict], int, bool, bool]:
     """no-speech skip (transcribe.py:308-321) then segment split; returns
-    (segments, new seek, skipped)."""
+    (segments, new seek, skipped, single_timestamp_ending).  Empty segments are not
+    cleared yet (word timestamps see them first, transcribe.py:412-499)."""
     thr_ns, thr_lp = st["thresholds"][2], st["thresholds"][1]
     if thr_ns is not None:
         skip = result.no_speech_prob > thr_ns
         if thr_lp is not None and result.avg_logprob > thr_lp:
             skip = False
         if skip:
-            return [], seek + segment_size, True
+            return [], seek + segment_size, True, False
     time_offset = float(seek * HOP_LENGTH / SAMPLE_RATE)
-    segs, new_seek = _split_segments(st["tokenizer"], result, seek, time_offset, segment_size,
-                                     segment_size * HOP_LENGTH / SAMPLE_RATE, st["input_stride"],
-                                     st["time_precision"])
-    return segs, new_seek, False
+    segs, new_seek, single_end = _split_segments(st["tokenizer"], result, seek, time_offset, segment_size,
+                                                 segment_size * HOP_LENGTH / SAMPLE_RATE, st["input_stride"],
+                                                 st["time_precision"])
+    return segs, new_seek, False, single_end
+
+
+def get_end(segments: List[dict]) -> Optional[float]:
+    """utils.py:78-82."""
+    return next((w["end"] for s in reversed(segments) for w in reversed(s.get("words", []))),
+                segments[-1]["end"] if segments else None)
+
+
+_PUNCTUATION = "\"'“¿([{-\"'.。,，!！?？:：”)]}、"  # transcribe.py:183
+
+
+def _word_anomaly_score(word: dict) -> float:
+    """transcribe.py:327-337."""
+    probability = word.get("probability", 0.0)
+    duration = word["end"] - word["start"]
+    score = 0.0
+    if probability < 0.15:
+        score += 1.0
+    if duration < 0.133:
+        score += (0.133 - duration) * 15
+    if duration > 2.0:
+        score += duration - 2.0
+    return score
+
+
+def _is_segment_anomaly(segment: Optional[dict]) -> bool:
+    """transcribe.py:339-345."""
+    if segment is None or not segment["words"]:
+        return False
+    words = [w for w in segment["words"] if w["word"] not in _PUNCTUATION]
+    words = words[:8]
+    score = sum(_word_anomaly_score(w) for w in words)
+    return score >= 3 or score + 0.01 >= len(words)
+
+
+def _next_words_segment(segments: List[dict]) -> Optional[dict]:
+    return next((s for s in segments if s["words"]), None)
+
+
+def _window_alignment(model, st, segs: List[dict], segment_size: int, slot: int):
+    """find_alignment of one window's segments (its audio features in `slot`)."""
+    tok = st["tokenizer"]
+    text_tokens = [t for s in segs for t in s["tokens"] if t < tok.eot]
+    return find_alignment(model, tok, text_tokens, segment_size, slot=slot)
+
+
+def _words_and_seek(st, segs, alignment, seek, previous_seek, segment_size, single_end, last_speech):
+    """transcribe.py:412-426 on a precomputed alignment: words of every segment, the
+    seek refinement from the last word; returns (seek, last_speech_timestamp)."""
+    apply_alignment(segs, copy.deepcopy(alignment), st["tokenizer"], st["prepend"], st["append"], last_speech)
+    time_offset = float(previous_seek * HOP_LENGTH / SAMPLE_RATE)
+    if not single_end:
+        last_word_end = get_end(segs)
+        if last_word_end is not None and last_word_end > time_offset:
+            seek = round(last_word_end * FRAMES_PER_SECOND)
+    return seek
 
 
 def _run_sequential(model, clips, initial_prompt_tokens, condition_on_previous_text, carry_initial_prompt, st):
@@ -259,6 +334,7 @@ def _run_sequential(model, clips, initial_prompt_tokens, condition_on_previous_t
     segments = []
     prompt_reset_since = 0
     remaining_prompt_length = model.dims.n_text_ctx // 2 - 1 - len(initial_prompt_tokens)
+    last_speech_timestamp = 0.0
     clip_idx, seek = 0, clips[0][0]
     while clip_idx < len(clips):
         cs, ce = clips[clip_idx]
@@ -281,9 +357,62 @@ def _run_sequential(model, clips, initial_prompt_tokens, condition_on_previous_t
         ctx.encode([seek], [segment_size])
         model._last_windows = ([seek], [segment_size])
         result = _decode_with_fallback(model, st["base"], st["temperatures"], [prompt or None], st["thresholds"])[0]
-        segs, seek, skipped = _apply_result(model, result, seek, segment_size, st)
+        previous_seek = seek
+        segs, seek, skipped, single_end = _apply_result(model, result, seek, segment_size, st)
         if skipped:
             continue
+        if st["word_timestamps"]:
+            if model._last_windows != ([previous_seek], [segment_size]):
+                ctx.encode([previous_seek], [segment_size])
+                model._last_windows = ([previous_seek], [segment_size])
+            alignment = _window_alignment(model, st, segs, segment_size, 0) if segs else []
+            seek = _words_and_seek(st, segs, alignment, seek, previous_seek, segment_size, single_end,
+                                   last_speech_timestamp)
+            time_offset = float(previous_seek * HOP_LENGTH / SAMPLE_RATE)
+            window_end_time = float((previous_seek + N_FRAMES) * HOP_LENGTH / SAMPLE_RATE)
+            segment_duration = segment_size * HOP_LENGTH / SAMPLE_RATE
+            threshold = st["hallucination"]
+            if threshold is not None:  # transcribe.py:428-484
+                if not single_end:
+                    last_word_end = get_end(segs)
+                    if last_word_end is not None and last_word_end > time_offset:
+                        remaining_duration = window_end_time - last_word_end
+                        if remaining_duration > threshold:
+                            seek = round(last_word_end * FRAMES_PER_SECOND)
+                        else:
+                            seek = previous_seek + segment_size
+                first_segment = _next_words_segment(segs)
+                if first_segment is not None and _is_segment_anomaly(first_segment):
+                    gap = first_segment["start"] - time_offset
+                    if gap > threshold:
+                        seek = previous_seek + round(gap * FRAMES_PER_SECOND)
+                        continue
+                hal_last_end = last_speech_timestamp
+                for si in range(len(segs)):
+                    segment = segs[si]
+                    if not segment["words"]:
+                        continue
+                    if _is_segment_anomaly(segment):
+                        next_segment = _next_words_segment(segs[si + 1:])
+                        if next_segment is not None:
+                            hal_next_start = next_segment["words"][0]["start"]
+                        else:
+                            hal_next_start = time_offset + segment_duration
+                        silence_before = (segment["start"] - hal_last_end > threshold
+                                          or segment["start"] < threshold or segment["start"] - time_offset < 2.0)
+                        silence_after = (hal_next_start - segment["end"] > threshold
+                                         or _is_segment_anomaly(next_segment) or window_end_time - segment["end"] < 2.0)
+                        if silence_before and silence_after:
+                            seek = round(max(time_offset + 1, segment["start"]) * FRAMES_PER_SECOND)
+                            if st["content_duration"] - segment["end"] < threshold:
+                                seek = content_frames
+                            segs[si:] = []
+                            break
+                    hal_last_end = segment["end"]
+            last_word_end = get_end(segs)
+            if last_word_end is not None:
+                last_speech_timestamp = last_word_end
+        _clear_empty(st["tokenizer"], segs)
         segments.extend(segs)
         all_tokens.extend(t for s in segs for t in s["tokens"])
         if not condition_on_previous_text or result.temperature > 0.5:
@@ -298,6 +427,8 @@ def _run_batched(model, clips, initial_prompt_tokens, st):
     seeks = [c[0] for c in clips]
     live = [True] * len(clips)
     per_clip: List[List[dict]] = [[] for _ in clips]
+    windows: List[List[tuple]] = [[] for _ in clips]  # word timestamps: per-window records
+    clip_speech = [0.0] * len(clips)
     first_window = True
     while any(live):
         batch = []  # (clip, seek, segment_size)
@@ -326,8 +457,45 @@ def _run_batched(model, clips, initial_prompt_tokens, st):
             ctx.encode([s for _, s, _ in chunk], [z for _, _, z in chunk])
             model._last_windows = ([s for _, s, _ in chunk], [z for _, _, z in chunk])
             results = _decode_with_fallback(model, st["base"], st["temperatures"], prompts, st["thresholds"])
-            for (ci, seek, segment_size), r in zip(chunk, results):
-                segs, new_seek, _ = _apply_result(model, r, seek, segment_size, st)
+            wins = ([s for _, s, _ in chunk], [z for _, _, z in chunk])
+            if st["word_timestamps"] and model._last_windows != wins:
+                ctx.encode(*wins)  # fallback re-encoded a subset: restore slot order
+                model._last_windows = wins
+            for slot, ((ci, seek, segment_size), r) in enumerate(zip(chunk, results)):
+                segs, new_seek, skipped, single_end = _apply_result(model, r, seek, segment_size, st)
+                if st["word_timestamps"] and not skipped:
+                    alignment = _window_alignment(model, st, segs, segment_size, slot) if segs else []
+                    # provisional: the clip-local running last-speech time (the true one,
+                    # from the preceding clips, is applied in the ordered pass below)
+                    new_seek = _words_and_seek(st, segs, alignment, new_seek, seek, segment_size, single_end,
+                                               clip_speech[ci])
+                    end = get_end(segs)
+                    if end is not None:
+                        clip_speech[ci] = end
+                    windows[ci].append((seek, segment_size, r, alignment, new_seek))
+                    segs = []
+                elif st["word_timestamps"]:
+                    windows[ci].append((seek, segment_size, r, None, new_seek))
+                _clear_empty(st["tokenizer"], segs)
                 per_clip[ci].extend(segs)
                 seeks[ci] = new_seek
-    return [s for clip in per_clip for s in clip]
+    if not st["word_timestamps"]:
+        return [s for clip in per_clip for s in clip]
+    # ordered pass: word timings with the running last_speech_timestamp of the
+    # reference's sequential loop (transcribe.py:271, 412-426, 485-486); a window whose
+    # seek would change under it makes the caller re-run the sequential schedule
+    out, last_speech = [], 0.0
+    for ci in range(len(clips)):
+        for seek, segment_size, r, alignment, prov_seek in windows[ci]:
+            if alignment is None:
+                continue
+            segs, new_seek, _, single_end = _apply_result(model, r, seek, segment_size, st)
+            new_seek = _words_and_seek(st, segs, alignment, new_seek, seek, segment_size, single_end, last_speech)
+            if new_seek != prov_seek:
+                return None
+            end = get_end(segs)
+            if end is not None:
+                last_speech = end
+            _clear_empty(st["tokenizer"], segs)
+            out.extend(segs)
+    return out
