@@ -42,6 +42,8 @@ def parse():
     p.add_argument("--max-windows", type=int, default=20)
     p.add_argument("--cpu-baseline", type=int, default=1)
     p.add_argument("--cpu-steps", type=int, default=6, help="decoder steps in the CPU baseline sample")
+    p.add_argument("--word-timestamps", type=int, default=0,
+                   help="config 5: transcribe(word_timestamps=True) (alignment + DTW on the GPU per window)")
     return p.parse_args()
 
 
@@ -165,6 +167,8 @@ def main():
     model = whisper.Whisper(whisper.ModelDimensions(**dims), args.model, device=local, dtype=args.dtype,
                             max_windows=args.max_windows, max_group=args.beam)
     model.load_state_dict(sd)
+    if args.model in whisper._ALIGNMENT_HEADS:  # as load_model does (reference __init__.py:176-177)
+        model.set_alignment_heads(whisper._ALIGNMENT_HEADS[args.model])
     if not (rank == 0 and world == 1 and args.cpu_baseline):
         del sd
         sd = None
@@ -178,11 +182,20 @@ def main():
     def reduce_max(x):
         return allreduce_max(pg, x)
 
+    if args.word_timestamps:
+        # word splitting needs token bytes; the box has no BPE rank file, so every text
+        # id decodes to its own word " w<id>" (host-side grouping only: the GPU work,
+        # first pass + alignment + DTW per window, is the same for any byte table)
+        from whisper import tokenizer as T
+        T.set_token_bytes("multilingual" if model.is_multilingual else "gpt2",
+                          {i: b" w%d" % i for i in range(dims["n_vocab"])})
+
     def one_step():
         # per-rank log-mel, global max over ranks (all-reduce MAX), normalize, transcribe
         return whisper.transcribe(model, dev_audio, temperature=0.0, beam_size=args.beam, language="en",
                                   condition_on_previous_text=False, clip_timestamps=clip_ts,
-                                  mel_max_reduce=reduce_max if pg is not None else None, schedule="batched")
+                                  mel_max_reduce=reduce_max if pg is not None else None, schedule="batched",
+                                  word_timestamps=bool(args.word_timestamps))
 
     for _ in range(args.warmup):
         one_step()
@@ -219,8 +232,8 @@ def main():
     tok = model.ctx.token_ms()
     p50_token_ms = float(np.median(tok)) if len(tok) else ms_per_token
 
-    # roofline of the dominant kernel (k_gemv_x: the split-K projection GEMVs of the
-    # decoder step, ~35% of step time), timed live with HIP events on the context's
+    # roofline of the dominant kernel (k_proj: the split-K projections of the decoder
+    # step, ~31% of step time over its three tile variants), timed live with HIP events on the context's
     # stream over launches at the bench batch (all layers, so weights stream from HBM)
     n_win = min(args.max_windows, n_clips)
     model.ctx.encode([3000 * i for i in range(n_win)], [3000] * n_win)
@@ -239,7 +252,7 @@ def main():
     def gbs(b, ms):
         return b / (ms * 1e-3) / 1e9
 
-    traffic = load_traffic("k_gemv_x")
+    traffic = load_traffic("k_proj")
     out = {
         "metric": "xRT (audio-s/s) large-v3 beam=5 @1/2/4/8 GPU; p50 per-token decode ms",
         "value": round(world * args.seconds * args.steps / elapsed_max, 3),
@@ -254,7 +267,8 @@ def main():
         "dtype": "fp16" if args.dtype == "fp16" else "f32",
         "data": "synthetic: seeded N(0,0.1^2)+440 Hz audio, seeded random-init weights at real dims",
         "config": {"workload": f"{args.model} beam={args.beam} transcribe(), {args.seconds:.0f} s audio per GPU, "
-                               f"30 s clip grid, condition_on_previous_text=False, temperature=0",
+                               f"30 s clip grid, condition_on_previous_text=False, temperature=0"
+                               + (", word_timestamps=True" if args.word_timestamps else ""),
                    "model": args.model, "global_batch": n_clips * world, "seq_len": 448,
                    "parallelism": f"windows sharded over {world} GPU(s), RCCL all-reduce(max)+gather"},
         "p50_token_ms": round(p50_token_ms, 4),
@@ -262,7 +276,7 @@ def main():
         "tokens_per_window": round(gathered[0][1] / max(1, n_clips), 1),
         "encoder_ms_per_window": round(enc_ms / max(enc_windows, 1), 3),
         "encoder_tflops": round(encoder_flops(dims) * enc_windows / (enc_ms * 1e-3) / 1e12, 1) if enc_ms else None,
-        "roofline": {"bound": "hbm", "kernel": f"k_gemv_x split-K projection GEMV ({rows} rows, avg of the six "
+        "roofline": {"bound": "hbm", "kernel": f"k_proj split-K projection ({rows} rows, avg of the six "
                                                 f"per decoder layer)",
                      "achieved": round(gbs(gemv_bytes, gemv_ms), 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(gbs(gemv_bytes, gemv_ms) / HBM_PEAK_GBS, 4),

@@ -133,7 +133,14 @@ int wh_prefill_logits(wh_ctx* ctx, int slot, const int* tokens, int n_tokens, fl
    entries of each (the rows of dtw(-matrix), timing.py:206). */
 int wh_align(wh_ctx* ctx, int slot, const int* tokens, int n_tokens, int n_sot, int num_frames, const int* align_heads,
              int n_align, int medfilt_width, float* token_probs, int* path, int* path_len);
-/* timing.dtw(x) of a host matrix x [n_rows][n_cols] (n_rows <= 1024) on the GPU:
+/* wh_align for n_win windows at once (slots[w], n_tokens[w] ids each, concatenated in
+   tokens; num_frames[w]): their first passes run batched (up to 1024 rows per pass) and
+   their DTWs run one workgroup per window in one launch.  Outputs concatenated in window
+   order: token_probs [T_w], paths [2][T_w + 1 + num_frames[w]/2], path_lens [n_win]. */
+int wh_align_batch(wh_ctx* ctx, int n_win, const int* slots, const int* tokens, const int* n_tokens, int n_sot,
+                   const int* num_frames, const int* align_heads, int n_align, int medfilt_width, float* token_probs,
+                   int* paths, int* path_lens);
+/* timing.dtw(x) of a host matrix x [n_rows][n_cols] (n_rows <= 1023) on the GPU:
    path [2][n_rows + n_cols], *path_len valid entries of each */
 int wh_dtw(wh_ctx* ctx, const float* x, int n_rows, int n_cols, int* path, int* path_len);
 

@@ -1,7 +1,7 @@
 """HBM traffic per launch of the decoder-step kernels from rocprofv3 PMC counters.
 
 Workload (`run`): large-v3 fp16 at the bench batch (20 windows x beam 5 = 100 rows),
-encode + decode_begin, then wh_time_stage 2 (the six split-K projection GEMVs of every
+encode + decode_begin, then wh_time_stage 2 (the six split-K projections (k_proj) of every
 decoder layer) and 3 (cross-attention of every layer) once each.
 
 Collected in two separate passes (FETCH_SIZE and WRITE_SIZE do not fit one TCC pass
@@ -30,7 +30,7 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 KERNELS = {
     # short name -> regex on the mangled kernel name
-    "k_gemv_x": r"k_gemv_xIDF16_Li7ELi7E",     # fp16, MT=7 (100 rows), EPI_PARTIAL
+    "k_proj": r"k_projIDF16_",                # fp16 split-K projections (all tile variants)
     "k_cross_attn": r"k_cross_attnIDF16_",
 }
 

@@ -138,3 +138,31 @@ def test_transcribe_word_timestamps(micro32, words_golden, run, schedule):
         for wa, wb in zip(a["words"], b["words"]):
             assert wa["start"] == pytest.approx(wb["start"]) and wa["end"] == pytest.approx(wb["end"])
             assert wa["probability"] == pytest.approx(wb["probability"], rel=1e-3)
+
+
+def test_align_batch_equals_single_windows(micro32, words_golden):
+    """wh_align_batch (first passes batched, one DTW workgroup per window) gives each
+    window exactly what wh_align gives it alone."""
+    import whisper
+    from whisper import synthetic as S
+    from whisper.timing import _alignment_head_ids
+    from whisper.tokenizer import get_tokenizer
+    m = micro32
+    audio = S.synthetic_audio(words_golden["audio_seconds"], seed=words_golden["audio_seed"])
+    mel = whisper.log_mel_spectrogram(audio, m.dims.n_mels, padding=whisper.audio.N_SAMPLES)
+    m.ctx.mel_write(mel)
+    seeks, segs = [0, 3000, 1234], [3000, 3000, 2500]
+    m.ctx.encode(seeks, segs)
+    m._last_windows = (seeks, segs)
+    tok = get_tokenizer(m.is_multilingual, num_languages=m.num_languages, language="en", task="transcribe")
+    rng = np.random.default_rng(11)
+    texts = [list(rng.integers(0, tok.eot, k)) for k in (5, 60, 23)]
+    seqs = [[*tok.sot_sequence, tok.no_timestamps, *t, tok.eot] for t in texts]
+    heads = _alignment_head_ids(m)
+    nfs = [3000, 2000, 2500]
+    batch = m.ctx.align_batch([0, 1, 2], seqs, len(tok.sot_sequence), nfs, heads)
+    for w in range(3):
+        one = m.ctx.align(w, seqs[w], len(tok.sot_sequence), nfs[w], heads)
+        np.testing.assert_allclose(batch[w][0], one[0], rtol=1e-5)
+        np.testing.assert_array_equal(batch[w][1], one[1])
+        np.testing.assert_array_equal(batch[w][2], one[2])

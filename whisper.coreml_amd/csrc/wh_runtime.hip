@@ -48,7 +48,7 @@ constexpr int CTX = 448;          // text positions (decoder.py:243, decoding.py
 constexpr int HCTX = CTX + 1;     // history capacity (tokens.shape[-1] may reach n_ctx + 1)
 constexpr int NSPLIT = 8;         // cross-attention key splits (1500 / 8 = 188 keys)
 constexpr int ENC_CHUNK = 16;     // encoder windows per pass
-constexpr int PRE_ROWS = 1024;    // prefill rows per pass
+constexpr int PRE_ROWS = 1024;    // min prefill rows per pass (the context sizes it to ~240 per window)
 constexpr int MROWS = 3008;       // melT rows per window (1 pad + 3000 + slack for padded conv1 K)
 constexpr int H1ROWS = 3002;      // conv1 output rows per window (zero rows 0 and 3001)
 constexpr int KC = 9;
@@ -110,6 +110,9 @@ struct wh_ctx {
   virtual int prefill_logits(int slot, const int* tokens, int n, float* logits, const int* ah, int na, float* aqk) = 0;
   virtual int align(int slot, const int* tokens, int n, int n_sot, int num_frames, const int* ah, int na, int medfilt,
                     float* probs, int* path, int* plen) = 0;
+  virtual int align_batch(int n_win, const int* slots, const int* tokens, const int* n_tokens, int n_sot,
+                          const int* num_frames, const int* ah, int na, int medfilt, float* probs, int* paths,
+                          int* plens) = 0;
   virtual int dtw(const float* x, int N, int M, int* path, int* plen) = 0;
   virtual int time_stage(int what, int iters, double* ms) = 0;
   std::vector<float> token_ms;  // per-token wall ms of each decode_steps chunk
@@ -163,6 +166,7 @@ struct Ctx : public wh_ctx {
   std::vector<T*> kc, vc;
   // decoder buffers
   int RD;
+  int PRE = PRE_ROWS;
   float *x_d, *po, *pm, *pl, *logits, *logits2, *nsp, *part;
   T *xn_d, *q_d, *att_d, *hm_d;
   int *row_tok, *row_pos, *row_win, *row_slot, *win_row0, *win_nrows, *win_slot, *rows_in, *src_rows;
@@ -259,7 +263,10 @@ struct Ctx : public wh_ctx {
     expected = 5 + La * 15 + 2 + 2 + Ld * 24 + 2;
     // ---------------- activations
     const int WE = std::min(Wcap, ENC_CHUNK);
-    RD = std::max(Wcap * Gcap, PRE_ROWS);
+    // first-pass rows per pass: every window's word-timestamp alignment (<= ~230 tokens)
+    // fits one pass, so its GEMMs run at M in the thousands
+    PRE = std::max(PRE_ROWS, std::min(Wcap * 240, 8192));
+    RD = std::max(Wcap * Gcap, PRE);
     const int LR = std::max(Wcap * Gcap, 2 * Wcap);
     size_t ab = 0;
     auto addA = [&](size_t bytes) { ab += ((bytes + 255) & ~size_t(255)) + 256; };
@@ -842,8 +849,8 @@ struct Ctx : public wh_ctx {
     // prefill runs with kv_beams = Gcap layout; rows use slot 0
     for (int w0 = 0; w0 < n_win;) {
       int rows = 0, nw = 0;
-      while (w0 + nw < n_win && (nw == 0 || rows + nin[w0 + nw] <= PRE_ROWS)) rows += nin[w0 + nw++];
-      if (rows > PRE_ROWS) return fail(-11, "prefill rows exceed buffer");
+      while (w0 + nw < n_win && (nw == 0 || rows + nin[w0 + nw] <= PRE)) rows += nin[w0 + nw++];
+      if (rows > PRE) return fail(-11, "prefill rows exceed buffer");
       std::vector<int> sub_toks(toks.begin() + (size_t)w0 * HCTX, toks.begin() + (size_t)(w0 + nw) * HCTX);
       std::vector<int> sub_n(nin.begin() + w0, nin.begin() + w0 + nw);
       TRY(prefill(w0, nw, sub_toks, sub_n, sot_index, true));
@@ -1038,67 +1045,152 @@ struct Ctx : public wh_ctx {
     return 0;
   }
 
-  // find_alignment's device half (timing.py:163-231): first pass over
-  // sot_sequence + [no_timestamps] + text + [eot] with the alignment heads' cross-QK,
-  // the text tokens' probabilities, the filtered head-mean matrix and its DTW path.
-  int align(int slot, const int* tokens, int n, int n_sot, int num_frames, const int* ah, int na, int medfilt,
-            float* probs, int* path, int* plen) override {
-    const int Tt = n - n_sot - 2, N = n - n_sot - 1, F = num_frames / 2;
-    if (n_sot < 1 || Tt < 1) return fail(-15, "align: need sot_sequence + no_timestamps + >= 1 text token + eot");
-    if (F < 1 || F > 1500) return fail(-15, "align: num_frames out of range");
+  // find_alignment's device half (timing.py:163-231) for a batch of windows: window w
+  // is sot_sequence + [no_timestamps] + text + [eot] (n_tokens[w] ids at tokens[sum of
+  // the previous n_tokens]) over the audio features of slots[w].  The windows' first
+  // passes run together (up to PRE rows per pass, cross-QK of the alignment
+  // heads captured), then the text tokens' probabilities, the filtered head-mean
+  // matrices and one DTW workgroup per window (all DTWs of a pass in one launch).
+  // Outputs are concatenated in window order: probs [T_w], paths [2][T_w+1+F_w],
+  // plens [n_win].
+  int align_batch(int n_win, const int* slots, const int* tokens, const int* n_tokens, int n_sot,
+                  const int* num_frames, const int* ah, int na, int medfilt, float* probs, int* paths,
+                  int* plens) override {
+    if (!finalized) return fail(-9, "weights not finalized");
+    if (n_win < 1) return fail(-15, "align: no windows");
     if (na < 1 || na > Ld * nh) return fail(-15, "align: alignment head count");
     if (medfilt < 1 || medfilt > 15 || medfilt % 2 == 0) return fail(-15, "align: medfilt_width must be odd <= 15");
-    const size_t b_qk = (size_t)na * n * 1500 * 4, b_lg = (size_t)std::min(Tt, 128) * V * 4,
-                 b_mat = (size_t)N * F * 4, b_tr = (size_t)(N + 1) * (F + 1), b_path = (size_t)2 * (N + F) * 4;
-    auto al = [](size_t b) { return (b + 255) & ~size_t(255); };
-    TRY(ensure_scratch(al(b_qk) + al(b_lg) + al(b_mat) + al(b_tr) + al(b_path) + 3 * al((size_t)Tt * 4 + 16)));
-    char* p = scratch;
-    float* d_qk = (float*)p; p += al(b_qk);
-    float* d_lg = (float*)p; p += al(b_lg);
-    float* d_mat = (float*)p; p += al(b_mat);
-    signed char* d_tr = (signed char*)p; p += al(b_tr);
-    int* d_path = (int*)p; p += al(b_path);
-    float* d_probs = (float*)p; p += al((size_t)Tt * 4 + 16);
-    int* d_tok = (int*)p; p += al((size_t)Tt * 4 + 16);
-    int* d_plen = (int*)p;
-    std::vector<std::vector<int>> keep;
-    TRY(first_pass(slot, tokens, n, ah, na, d_qk, keep));
-    // logits of the rows that predict the text tokens, 128 rows at a time
-    std::vector<int> sel(Tt);
-    for (int k = 0; k < Tt; ++k) sel[k] = n_sot + k;
-    HIPCHK(hipMemcpyAsync(d_tok, tokens + n_sot + 1, Tt * 4, hipMemcpyHostToDevice, st));
-    for (int r0 = 0; r0 < Tt; r0 += 128) {
-      const int rr = std::min(128, Tt - r0);
-      HIPCHK(hipMemcpyAsync(rows_in, sel.data() + r0, rr * 4, hipMemcpyHostToDevice, st));
-      TRY(vocab(rows_in, rr, d_lg));
-      launch_token_probs(d_lg, V, 0, rr, tokens[n - 1], d_tok + r0, d_probs + r0, st);
-      HIPCHK(hipStreamSynchronize(st));  // rows_in / d_lg are reused by the next chunk
+    std::vector<int64_t> tok_off(n_win + 1, 0), prob_off(n_win + 1, 0), path_off(n_win + 1, 0), mat_off(n_win + 1, 0),
+        tr_off(n_win + 1, 0);
+    int rows_max = 0;
+    for (int w = 0; w < n_win; ++w) {
+      const int n = n_tokens[w], Tt = n - n_sot - 2, F = num_frames[w] / 2;
+      if (n_sot < 1 || Tt < 1) return fail(-15, "align: need sot_sequence + no_timestamps + >= 1 text token + eot");
+      if (n > CTX) return fail(-15, "align: more than 448 tokens");
+      if (F < 1 || F > 1500) return fail(-15, "align: num_frames out of range");
+      if (slots[w] < 0 || slots[w] >= Wcap) return fail(-15, "align: bad slot");
+      const int N = Tt + 1;
+      tok_off[w + 1] = tok_off[w] + n;
+      prob_off[w + 1] = prob_off[w] + Tt;
+      path_off[w + 1] = path_off[w] + 2 * (N + F);
+      mat_off[w + 1] = mat_off[w] + ((int64_t)N * F + 63) / 64 * 64;
+      tr_off[w + 1] = tr_off[w] + (dtw_trace_bytes(N, F) + 255) / 256 * 256;
+      rows_max = std::max(rows_max, n);
     }
-    launch_align_matrix(d_qk, n, 1500, F, na, n_sot, N, medfilt, d_mat, st);
-    if (launch_dtw(d_mat, N, F, -1.f, d_tr, d_path, d_plen, st)) return fail(-15, "align: too many token rows");
-    HIPCHK(hipMemcpyAsync(probs, d_probs, Tt * 4, hipMemcpyDeviceToHost, st));
-    HIPCHK(hipMemcpyAsync(plen, d_plen, 4, hipMemcpyDeviceToHost, st));
-    HIPCHK(hipMemcpyAsync(path, d_path, b_path, hipMemcpyDeviceToHost, st));
+    // pass grouping: consecutive windows while the rows fit PRE and the cross-QK budget
+    const int64_t qk_row = (int64_t)na * 1500 * 4;
+    const int cap = (int)std::max<int64_t>(rows_max, std::min<int64_t>(PRE, ((int64_t)1 << 30) / qk_row));
+    auto al = [](size_t b) { return (b + 255) & ~size_t(255); };
+    const size_t b_qk = al((size_t)qk_row * cap), b_lg = al((size_t)128 * V * 4), b_mat = al(mat_off[n_win] * 4),
+                 b_tr = al(tr_off[n_win]), b_path = al(path_off[n_win] * 4), b_pr = al(prob_off[n_win] * 4 + 16),
+                 b_pl = al((size_t)n_win * 4), b_jobs = al((size_t)n_win * sizeof(DtwJob));
+    TRY(ensure_scratch(b_qk + b_lg + b_mat + b_tr + b_path + 2 * b_pr + b_pl + b_jobs));
+    char* p = scratch;
+    float* d_qk = (float*)p; p += b_qk;
+    float* d_lg = (float*)p; p += b_lg;
+    float* d_mat = (float*)p; p += b_mat;
+    char* d_tr = p; p += b_tr;
+    int* d_path = (int*)p; p += b_path;
+    float* d_probs = (float*)p; p += b_pr;
+    int* d_ptok = (int*)p; p += b_pr;
+    int* d_plen = (int*)p; p += b_pl;
+    DtwJob* d_jobs = (DtwJob*)p;
+
+    // token of every probability row (timing.py:191: text_tokens[k])
+    std::vector<int> ptok(prob_off[n_win]);
+    for (int w = 0; w < n_win; ++w)
+      for (int k = 0; k < prob_off[w + 1] - prob_off[w]; ++k) ptok[prob_off[w] + k] = tokens[tok_off[w] + n_sot + 1 + k];
+    HIPCHK(hipMemcpyAsync(d_ptok, ptok.data(), ptok.size() * 4, hipMemcpyHostToDevice, st));
+    std::vector<int> map((size_t)Ld * nh, -1);
+    for (int i = 0; i < na; ++i)
+      if (ah[i] >= 0 && ah[i] < Ld * nh) map[ah[i]] = i;
+    HIPCHK(hipMemcpyAsync(qk_map, map.data(), map.size() * 4, hipMemcpyHostToDevice, st));
+    std::vector<DtwJob> jobs(n_win);
+    std::vector<int> anc0((size_t)CTX, 0);
+    const int eot = tokens[tok_off[1] - 1];
+    for (int w0 = 0; w0 < n_win;) {
+      int nw = 0, R = 0;
+      while (w0 + nw < n_win && (nw == 0 || R + n_tokens[w0 + nw] <= cap)) R += n_tokens[w0 + nw++];
+      // rows of this pass: window slot, beam slot 0, position
+      std::vector<int> rt(R), rp(R), rw(R), rs(R, 0), wr0(nw), wnr(nw), wsl(nw), sel;
+      int r = 0;
+      for (int i = 0; i < nw; ++i) {
+        const int w = w0 + i, n = n_tokens[w];
+        wr0[i] = r; wnr[i] = n; wsl[i] = slots[w];
+        for (int q = 0; q < n; ++q, ++r) { rt[r] = tokens[tok_off[w] + q]; rp[r] = q; rw[r] = slots[w]; }
+        for (int k = 0; k < n - n_sot - 2; ++k) sel.push_back(wr0[i] + n_sot + k);
+        if (tokens[tok_off[w] + n - 1] != eot) return fail(-15, "align: windows must end with the same eot");
+        HIPCHK(hipMemcpyAsync(S.anc + (size_t)slots[w] * CTX, anc0.data(), CTX * 4, hipMemcpyHostToDevice, st));
+      }
+      for (int q = 0; q < R; ++q)
+        if (rt[q] < 0 || rt[q] >= V) return fail(-15, "align: token out of vocabulary");
+      HIPCHK(hipMemcpyAsync(row_tok, rt.data(), R * 4, hipMemcpyHostToDevice, st));
+      HIPCHK(hipMemcpyAsync(row_pos, rp.data(), R * 4, hipMemcpyHostToDevice, st));
+      HIPCHK(hipMemcpyAsync(row_win, rw.data(), R * 4, hipMemcpyHostToDevice, st));
+      HIPCHK(hipMemcpyAsync(row_slot, rs.data(), R * 4, hipMemcpyHostToDevice, st));
+      HIPCHK(hipMemcpyAsync(win_row0, wr0.data(), nw * 4, hipMemcpyHostToDevice, st));
+      HIPCHK(hipMemcpyAsync(win_nrows, wnr.data(), nw * 4, hipMemcpyHostToDevice, st));
+      HIPCHK(hipMemcpyAsync(win_slot, wsl.data(), nw * 4, hipMemcpyHostToDevice, st));
+      launch_embed<T>(E, Pdec, ns, row_tok, row_pos, nullptr, nullptr, 1, HCTX, CTX - 1, x_d, R, st);
+      TRY(dec_layers(R, row_win, row_slot, row_pos, 1, nw, win_row0, win_nrows, win_slot, d_qk, qk_map, R));
+      // probabilities of the text tokens, 128 logit rows at a time
+      const int64_t pb = prob_off[w0];
+      for (int c0 = 0; c0 < (int)sel.size(); c0 += 128) {
+        const int rr = std::min<int>(128, (int)sel.size() - c0);
+        HIPCHK(hipMemcpyAsync(rows_in, sel.data() + c0, rr * 4, hipMemcpyHostToDevice, st));
+        TRY(vocab(rows_in, rr, d_lg));
+        launch_token_probs(d_lg, V, rr, eot, d_ptok + pb + c0, d_probs + pb + c0, st);
+      }
+      for (int i = 0; i < nw; ++i) {
+        const int w = w0 + i, N = n_tokens[w] - n_sot - 1, F = num_frames[w] / 2;
+        float* mat = d_mat + mat_off[w];
+        launch_align_matrix(d_qk + (int64_t)wr0[i] * 1500, (int64_t)R * 1500, n_tokens[w], 1500, F, na, n_sot, N,
+                            medfilt, mat, st);
+        jobs[w] = DtwJob{mat, (unsigned*)(d_tr + tr_off[w]), d_path + path_off[w], d_plen + w, N, F, 0};
+      }
+      size_t lds = 0;
+      if (dtw_prepare(jobs.data() + w0, nw, &lds)) return fail(-15, "align: DTW shape");
+      HIPCHK(hipMemcpyAsync(d_jobs + w0, jobs.data() + w0, nw * sizeof(DtwJob), hipMemcpyHostToDevice, st));
+      int max_n = 0;
+      for (int i = 0; i < nw; ++i) max_n = std::max(max_n, jobs[w0 + i].N);
+      if (launch_dtw_jobs(d_jobs + w0, nw, max_n, jobs[w0].in_lds, lds, -1.f, st))
+        return fail(-15, "align: DTW launch");
+      HIPCHK(hipStreamSynchronize(st));  // host row vectors of this pass go out of scope
+      w0 += nw;
+    }
+    HIPCHK(hipMemcpyAsync(probs, d_probs, prob_off[n_win] * 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(plens, d_plen, n_win * 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(paths, d_path, path_off[n_win] * 4, hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
     HIPCHK(hipGetLastError());
     return 0;
   }
 
+  int align(int slot, const int* tokens, int n, int n_sot, int num_frames, const int* ah, int na, int medfilt,
+            float* probs, int* path, int* plen) override {
+    return align_batch(1, &slot, tokens, &n, n_sot, &num_frames, ah, na, medfilt, probs, path, plen);
+  }
+
   // timing.dtw (timing.py:82-105, 139-151) of a host cost matrix x [N][M] on the GPU
   int dtw(const float* x, int N, int M, int* path, int* plen) override {
-    if (N < 1 || M < 1 || N > 1024 || (int64_t)N * M > (int64_t)1 << 26) return fail(-15, "dtw: shape out of range");
+    if (N < 1 || M < 1 || N > 1023 || (int64_t)N * M > (int64_t)1 << 26) return fail(-15, "dtw: shape out of range");
     auto al = [](size_t b) { return (b + 255) & ~size_t(255); };
-    const size_t b_x = (size_t)N * M * 4, b_tr = (size_t)(N + 1) * (M + 1), b_path = (size_t)2 * (N + M) * 4;
-    TRY(ensure_scratch(al(b_x) + al(b_tr) + al(b_path) + 256));
+    const size_t b_x = al((size_t)N * M * 4), b_tr = al(dtw_trace_bytes(N, M)), b_path = al((size_t)2 * (N + M) * 4);
+    TRY(ensure_scratch(b_x + b_tr + b_path + 256 + al(sizeof(DtwJob))));
     char* p = scratch;
-    float* d_x = (float*)p; p += al(b_x);
-    signed char* d_tr = (signed char*)p; p += al(b_tr);
-    int* d_path = (int*)p; p += al(b_path);
-    int* d_plen = (int*)p;
-    HIPCHK(hipMemcpyAsync(d_x, x, b_x, hipMemcpyHostToDevice, st));
-    TRY(launch_dtw(d_x, N, M, 1.f, d_tr, d_path, d_plen, st) ? fail(-15, "dtw launch") : 0);
+    float* d_x = (float*)p; p += b_x;
+    unsigned* d_tr = (unsigned*)p; p += b_tr;
+    int* d_path = (int*)p; p += b_path;
+    int* d_plen = (int*)p; p += 256;
+    DtwJob* d_job = (DtwJob*)p;
+    DtwJob job{d_x, d_tr, d_path, d_plen, N, M, 0};
+    size_t lds = 0;
+    if (dtw_prepare(&job, 1, &lds)) return fail(-15, "dtw: shape");
+    HIPCHK(hipMemcpyAsync(d_x, x, (size_t)N * M * 4, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(d_job, &job, sizeof(job), hipMemcpyHostToDevice, st));
+    if (launch_dtw_jobs(d_job, 1, N, job.in_lds, lds, 1.f, st)) return fail(-15, "dtw launch");
     HIPCHK(hipMemcpyAsync(plen, d_plen, 4, hipMemcpyDeviceToHost, st));
-    HIPCHK(hipMemcpyAsync(path, d_path, b_path, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(path, d_path, (size_t)2 * (N + M) * 4, hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
     HIPCHK(hipGetLastError());
     return 0;
@@ -1301,6 +1393,12 @@ int wh_align(wh_ctx* ctx, int slot, const int* tokens, int n_tokens, int n_sot, 
              int n_align, int medfilt_width, float* token_probs, int* path, int* path_len) {
   CTXCALL(ctx->align(slot, tokens, n_tokens, n_sot, num_frames, align_heads, n_align, medfilt_width, token_probs, path,
                      path_len));
+}
+int wh_align_batch(wh_ctx* ctx, int n_win, const int* slots, const int* tokens, const int* n_tokens, int n_sot,
+                   const int* num_frames, const int* align_heads, int n_align, int medfilt_width, float* token_probs,
+                   int* paths, int* path_lens) {
+  CTXCALL(ctx->align_batch(n_win, slots, tokens, n_tokens, n_sot, num_frames, align_heads, n_align, medfilt_width,
+                           token_probs, paths, path_lens));
 }
 int wh_dtw(wh_ctx* ctx, const float* x, int n_rows, int n_cols, int* path, int* path_len) {
   CTXCALL(ctx->dtw(x, n_rows, n_cols, path, path_len));

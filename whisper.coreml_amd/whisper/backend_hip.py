@@ -69,6 +69,8 @@ _EXPORTS = {
     "wh_prefill_logits": (c_int, [c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p]),
     "wh_align": (c_int, [c_void_p, c_int, c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_int, c_void_p, c_void_p,
                          POINTER(c_int)]),
+    "wh_align_batch": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int,
+                               c_int, c_void_p, c_void_p, c_void_p]),
     "wh_dtw": (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p, POINTER(c_int)]),
     "wh_stats": (c_int, [c_void_p, POINTER(c_double), c_int]),
     "wh_sync": (c_int, [c_void_p]),
@@ -274,16 +276,33 @@ class HipContext:
               medfilt_width: int = 7):
         """find_alignment's device half (timing.py:163-231): returns (text_token_probs [T],
         text_indices, time_indices) of dtw(-matrix)."""
-        t = np.ascontiguousarray(tokens, dtype=np.int32)
+        return self.align_batch([slot], [tokens], n_sot, [num_frames], align_heads, medfilt_width)[0]
+
+    def align_batch(self, slots: Sequence[int], token_lists: Sequence[Sequence[int]], n_sot: int,
+                    num_frames: Sequence[int], align_heads: Sequence[int], medfilt_width: int = 7):
+        """wh_align_batch: one (probs, text_indices, time_indices) per window."""
+        n = len(slots)
+        toks = np.ascontiguousarray(np.concatenate([np.asarray(t, dtype=np.int32) for t in token_lists]))
+        ntok = np.asarray([len(t) for t in token_lists], dtype=np.int32)
+        nfr = np.asarray(num_frames, dtype=np.int32)
+        sl = np.asarray(slots, dtype=np.int32)
         ah = np.ascontiguousarray(align_heads, dtype=np.int32)
-        T = len(t) - n_sot - 2
-        probs = np.zeros(max(T, 1), dtype=np.float32)
-        width = (T + 1) + num_frames // 2
-        path = np.zeros((2, width), dtype=np.int32)
-        n = c_int(0)
-        self._check(self.lib.wh_align(self.h, slot, _ptr(t), len(t), n_sot, num_frames, _ptr(ah), len(ah),
-                                      medfilt_width, _ptr(probs), _ptr(path), ctypes.byref(n)), "wh_align")
-        return probs[:T], path[0, :n.value].copy(), path[1, :n.value].copy()
+        T = ntok - n_sot - 2
+        widths = (T + 1) + nfr // 2
+        probs = np.zeros(max(int(T.sum()), 1), dtype=np.float32)
+        paths = np.zeros(max(int(2 * widths.sum()), 1), dtype=np.int32)
+        plens = np.zeros(n, dtype=np.int32)
+        self._check(self.lib.wh_align_batch(self.h, n, _ptr(sl), _ptr(toks), _ptr(ntok), n_sot, _ptr(nfr), _ptr(ah),
+                                            len(ah), medfilt_width, _ptr(probs), _ptr(paths), _ptr(plens)),
+                    "wh_align_batch")
+        out, po, qo = [], 0, 0
+        for w in range(n):
+            L, W = int(plens[w]), int(widths[w])
+            path = paths[qo:qo + 2 * W].reshape(2, W)
+            out.append((probs[po:po + T[w]].copy(), path[0, :L].copy(), path[1, :L].copy()))
+            po += int(T[w])
+            qo += 2 * W
+        return out
 
     def dtw(self, x: np.ndarray) -> np.ndarray:
         """timing.dtw(x) on the GPU: [2][path length] (text indices, time indices)."""

@@ -46,15 +46,33 @@ def find_alignment(model: "Whisper", tokenizer: Tokenizer, text_tokens: List[int
                    medfilt_width: int = 7, qk_scale: float = 1.0, slot: int = 0) -> List[WordTiming]:
     """timing.py:163-231.  `slot` names the context slot holding the window's audio
     features (the reference uses the model's cached cross-KV of the last window)."""
-    if len(text_tokens) == 0:
-        return []
+    return find_alignment_batch(model, tokenizer, [text_tokens], [num_frames], [slot], medfilt_width=medfilt_width,
+                                qk_scale=qk_scale)[0]
+
+
+def find_alignment_batch(model: "Whisper", tokenizer: Tokenizer, text_tokens: List[List[int]],
+                         num_frames: List[int], slots: List[int], *, medfilt_width: int = 7,
+                         qk_scale: float = 1.0) -> List[List[WordTiming]]:
+    """find_alignment of several windows (slots) with one wh_align_batch call: their
+    first passes batched on the GPU, one DTW workgroup per window."""
     if qk_scale != 1.0:
         raise NotImplementedError("qk_scale != 1.0 (the reference always passes 1.0)")
-    tokens = [*tokenizer.sot_sequence, tokenizer.no_timestamps, *text_tokens, tokenizer.eot]
-    text_token_probs, text_indices, time_indices = model.ctx.align(
-        slot, tokens, len(tokenizer.sot_sequence), num_frames, _alignment_head_ids(model), medfilt_width)
-    text_token_probs = text_token_probs.astype(np.float64).tolist()
+    out: List[List[WordTiming]] = [[] for _ in text_tokens]
+    todo = [i for i, t in enumerate(text_tokens) if len(t) > 0]
+    if not todo:
+        return out
+    seqs = [[*tokenizer.sot_sequence, tokenizer.no_timestamps, *text_tokens[i], tokenizer.eot] for i in todo]
+    res = model.ctx.align_batch([slots[i] for i in todo], seqs, len(tokenizer.sot_sequence),
+                                [num_frames[i] for i in todo], _alignment_head_ids(model), medfilt_width)
+    for i, (probs, text_indices, time_indices) in zip(todo, res):
+        out[i] = _words_from_path(tokenizer, text_tokens[i], probs, text_indices, time_indices)
+    return out
 
+
+def _words_from_path(tokenizer: Tokenizer, text_tokens: List[int], probs: np.ndarray, text_indices: np.ndarray,
+                     time_indices: np.ndarray) -> List[WordTiming]:
+    """timing.py:208-231 on the device results."""
+    text_token_probs = probs.astype(np.float64).tolist()
     words, word_tokens = tokenizer.split_to_word_tokens(text_tokens + [tokenizer.eot])
     if len(word_tokens) <= 1:
         return []

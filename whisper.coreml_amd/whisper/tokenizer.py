@@ -173,11 +173,15 @@ class Tokenizer:
 
     def decode_with_timestamps(self, token_ids: List[int]) -> str:
         ranks = _ranks(self.encoding_name) or {}
-        inv = {v: k for k, v in self.special_tokens.items()}
-        out = b""
-        for t in token_ids:
-            out += ranks[t] if t in ranks else inv.get(t, "").encode()
-        return out.decode("utf-8", errors="replace")
+        inv = self._special_bytes()
+        return b"".join(ranks[t] if t in ranks else inv.get(t, b"") for t in token_ids).decode("utf-8", errors="replace")
+
+    def _special_bytes(self) -> Dict[int, bytes]:
+        inv = self.__dict__.get("_inv_special")
+        if inv is None:
+            inv = {v: k.encode() for k, v in self.special_tokens.items()}
+            self.__dict__["_inv_special"] = inv
+        return inv
 
     # word splitting for word-level timestamps (tokenizer.py:277-327)
     def split_to_word_tokens(self, tokens: List[int]):

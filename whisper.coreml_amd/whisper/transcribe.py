@@ -33,7 +33,7 @@ import numpy as np
 from .audio import FRAMES_PER_SECOND, HOP_LENGTH, N_FRAMES, N_SAMPLES, SAMPLE_RATE, load_audio
 from .backend_hip import DeviceAudio
 from .decoding import DecodingOptions, DecodingResult, detect_language, run_windows
-from .timing import apply_alignment, find_alignment
+from .timing import apply_alignment, find_alignment, find_alignment_batch
 from .tokenizer import LANGUAGES, get_tokenizer
 
 if TYPE_CHECKING:
@@ -461,10 +461,17 @@ def _run_batched(model, clips, initial_prompt_tokens, st):
             if st["word_timestamps"] and model._last_windows != wins:
                 ctx.encode(*wins)  # fallback re-encoded a subset: restore slot order
                 model._last_windows = wins
+            applied = [_apply_result(model, r, seek, segment_size, st) for (ci, seek, segment_size), r in
+                       zip(chunk, results)]
+            if st["word_timestamps"]:
+                # every window's alignment of this chunk in one batched device call
+                tok = st["tokenizer"]
+                texts = [[t for s_ in a[0] for t in s_["tokens"] if t < tok.eot] for a in applied]
+                aligns = find_alignment_batch(model, tok, texts, [z for _, _, z in chunk], list(range(len(chunk))))
             for slot, ((ci, seek, segment_size), r) in enumerate(zip(chunk, results)):
-                segs, new_seek, skipped, single_end = _apply_result(model, r, seek, segment_size, st)
+                segs, new_seek, skipped, single_end = applied[slot]
                 if st["word_timestamps"] and not skipped:
-                    alignment = _window_alignment(model, st, segs, segment_size, slot) if segs else []
+                    alignment = aligns[slot]
                     # provisional: the clip-local running last-speech time (the true one,
                     # from the preceding clips, is applied in the ordered pass below)
                     new_seek = _words_and_seek(st, segs, alignment, new_seek, seek, segment_size, single_end,
