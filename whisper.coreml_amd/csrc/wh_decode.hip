@@ -14,6 +14,7 @@ namespace wh {
 
 constexpr int LR_THREADS = 1024;
 constexpr int KC = 9;       // candidates kept per row (beam + 1 <= 9)
+constexpr int LU = 13;      // row loads in flight per thread per batch (13 x 1024 >= V / 4)
 
 struct BlockRed {
   float v[16];
@@ -77,16 +78,28 @@ __global__ __launch_bounds__(LR_THREADS) void k_logit_rows(float* __restrict__ l
   const int len = s.len[w], sb = s.sample_begin[w];
   const int* hist = s.hist + (int64_t)r * s.hctx;
   const int V = o.V, tb = o.ts_begin;
+  // last timestamp token of the sampled part (decoding.py:503-508): every lane checks
+  // its positions, the block takes the largest (a backward scan by one lane would put
+  // one memory latency per sampled token on every step)
+  __shared__ int pmax_w[LR_THREADS / 64];
+  {
+    int pm = -1;
+    for (int p = sb + tid; p < len; p += LR_THREADS)
+      if (hist[p] >= tb) pm = p;
+#pragma unroll
+    for (int o2 = 32; o2 > 0; o2 >>= 1) pm = max(pm, __shfl_xor(pm, o2, 64));
+    if ((tid & 63) == 0) pmax_w[tid >> 6] = pm;
+  }
+  __syncthreads();
   if (tid == 0) {
     const int nseq = len - sb;
     const int last_ts = nseq >= 1 && hist[len - 1] >= tb;
     const int penult_ts = nseq < 2 || hist[len - 2] >= tb;
-    int ts_last = -1;
-    for (int p = len - 1; p >= sb; --p)
-      if (hist[p] >= tb) { ts_last = hist[p]; break; }
+    int pm = -1;
+    for (int k = 0; k < LR_THREADS / 64; ++k) pm = max(pm, pmax_w[k]);
     info[0] = last_ts;
     info[1] = penult_ts;
-    info[2] = ts_last;
+    info[2] = pm >= 0 ? hist[pm] : -1;
     info[3] = (len == sb);
   }
   __syncthreads();
@@ -110,67 +123,81 @@ __global__ __launch_bounds__(LR_THREADS) void k_logit_rows(float* __restrict__ l
   }
   float* row = logits + (int64_t)r * ldl;
   const bool sb_first = first && o.suppress_blank;
-  // the filters are applied once, in place (the logits are this step's scratch); every
-  // later pass re-reads the filtered row from L2 (it does not fit registers or LDS)
-  {
-    constexpr int U = 8;
-    for (int i0 = tid; i0 < V; i0 += LR_THREADS * U) {
-      float v[U];
+  // every pass reads the row in batches of LU loads per thread, all in flight before
+  // the first use (a load-use chain per element would put one memory latency on each
+  // of a thread's ~51 elements)
+#define ROW_PASS(KILLTEXT, BODY)                                                  \
+  for (int i0 = tid; i0 < V; i0 += LR_THREADS * LU) {                            \
+    float vv[LU];                                                                \
+    _Pragma("unroll") for (int u = 0; u < LU; ++u) {                             \
+      const int i_ = i0 + LR_THREADS * u;                                        \
+      vv[u] = i_ < V ? row[i_] : -INFINITY;                                      \
+    }                                                                            \
+    _Pragma("unroll") for (int u = 0; u < LU; ++u) {                             \
+      const int i = i0 + LR_THREADS * u;                                         \
+      if (i < V) {                                                               \
+        const float x = ((KILLTEXT) && i < tb) ? -INFINITY : vv[u];              \
+        BODY                                                                     \
+      }                                                                          \
+    }                                                                            \
+  }
+  // pass A: the filters, applied once in place (the logits are this step's scratch),
+  // and the maxima the later passes need: m over all, and over text / timestamp ids
+  // (log-probabilities are monotone in the logit, so their maxima follow exactly)
+  float m = -INFINITY, mx_ts = -INFINITY, mx_tx = -INFINITY;
+  for (int i0 = tid; i0 < V; i0 += LR_THREADS * LU) {
+    float vv[LU];
+    unsigned sw[LU];
 #pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const int i = i0 + LR_THREADS * u;
-        v[u] = i < V ? row[i] : 0.f;
-      }
+    for (int u = 0; u < LU; ++u) {
+      const int i = i0 + LR_THREADS * u;
+      vv[u] = i < V ? row[i] : -INFINITY;
+      sw[u] = (o.suppress && i < V) ? o.suppress[i >> 5] : 0u;
+    }
 #pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const int i = i0 + LR_THREADS * u;
-        if (i >= V) continue;
-        bool kill = false;
-        if (sb_first)
-          for (int b = 0; b < o.n_blank; ++b) kill |= (i == o.blank[b]);
-        if (o.suppress && ((o.suppress[i >> 5] >> (i & 31)) & 1u)) kill = true;
-        if (o.timestamps) {
-          kill |= (i == o.no_ts);
-          for (int q = 0; q < nm; ++q) kill |= (i >= mlo[q] && i < mhi[q]);
-        }
-        if (kill) row[i] = -INFINITY;
+    for (int u = 0; u < LU; ++u) {
+      const int i = i0 + LR_THREADS * u;
+      if (i >= V) continue;
+      bool kill = (sw[u] >> (i & 31)) & 1u;
+      if (sb_first)
+        for (int b = 0; b < o.n_blank; ++b) kill |= (i == o.blank[b]);
+      if (o.timestamps) {
+        kill |= (i == o.no_ts);
+        for (int q = 0; q < nm; ++q) kill |= (i >= mlo[q] && i < mhi[q]);
       }
+      float x = vv[u];
+      if (kill) {
+        x = -INFINITY;
+        row[i] = -INFINITY;
+      }
+      m = fmaxf(m, x);
+      if (i >= tb) mx_ts = fmaxf(mx_ts, x);
+      else mx_tx = fmaxf(mx_tx, x);
     }
   }
-  __syncthreads();
-  auto val = [&](int i) -> float { return row[i]; };
+  m = block_max(m, sm);
   bool text_killed = false;
   if (o.timestamps) {
-    // ApplyTimestampRules tail: if logsumexp(logprobs[tb:]) > max(logprobs[:tb]) mask text
-    float m = -INFINITY;
-    for (int i = tid; i < V; i += LR_THREADS) m = fmaxf(m, val(i));
-    m = block_max(m, sm);
+    // ApplyTimestampRules tail (decoding.py:522-531): if logsumexp(logprobs[tb:]) >
+    // max(logprobs[:tb]) mask the text tokens
+    mx_ts = block_max(mx_ts, sm);
+    mx_tx = block_max(mx_tx, sm);
     float se = 0.f;
-    for (int i = tid; i < V; i += LR_THREADS) se += __expf(val(i) - m);
+    ROW_PASS(false, se += __expf(x - m);)
     const float lS0 = logf(block_sum(se, sm));
-    float mts = -INFINITY, mtx = -INFINITY;
-    for (int i = tid; i < V; i += LR_THREADS) {
-      const float lp = (val(i) - m) - lS0;
-      if (i >= tb) mts = fmaxf(mts, lp);
-      else mtx = fmaxf(mtx, lp);
-    }
-    mts = block_max(mts, sm);
-    mtx = block_max(mtx, sm);
+    const float mts = mx_ts > -INFINITY ? (mx_ts - m) - lS0 : -INFINITY;
+    const float mtx = mx_tx > -INFINITY ? (mx_tx - m) - lS0 : -INFINITY;
     float st = 0.f;
-    if (mts > -INFINITY)
-      for (int i = tb + tid; i < V; i += LR_THREADS) st += __expf(((val(i) - m) - lS0) - mts);
+    if (mts > -INFINITY) {
+      ROW_PASS(false, if (i >= tb) st += __expf(((x - m) - lS0) - mts);)
+    }
     st = block_sum(st, sm);
     const float ts_lp = mts > -INFINITY ? mts + logf(st) : -INFINITY;
     text_killed = ts_lp > mtx;
+    if (text_killed) m = mx_ts;  // the max of what is left
   }
-  auto fval = [&](int i) -> float { return (text_killed && i < tb) ? -INFINITY : val(i); };
-  // final log_softmax
-  float m = -INFINITY;
-  for (int i = tid; i < V; i += LR_THREADS) m = fmaxf(m, fval(i));
-  m = block_max(m, sm);
+  // final log_softmax normaliser, fused with the token choice (which does not need it)
   float se = 0.f;
-  for (int i = tid; i < V; i += LR_THREADS) se += __expf(fval(i) - m);
-  const float logS = logf(block_sum(se, sm));
   float* cv = s.cand_val + (int64_t)r * KC;
   int* ci = s.cand_idx + (int64_t)r * KC;
   if (!o.beam) {
@@ -178,20 +205,22 @@ __global__ __launch_bounds__(LR_THREADS) void k_logit_rows(float* __restrict__ l
     int bi = 0x7fffffff;
     if (o.temperature > 0.f) {
       const unsigned long long key = splitmix64(o.seed ^ ((unsigned long long)r << 40) ^ ((unsigned long long)len << 20));
-      for (int i = tid; i < V; i += LR_THREADS) {
-        const float xv = fval(i);
-        if (xv == -INFINITY) continue;
-        const unsigned long long z = splitmix64(key + (unsigned long long)i);
-        const float u = ((float)(z >> 40) + 0.5f) * (1.0f / 16777216.0f);
-        const float gsc = xv / o.temperature - logf(-logf(u));
-        if (better(gsc, i, bv, bi)) { bv = gsc; bi = i; bx = xv; }
-      }
+      ROW_PASS(text_killed, {
+        se += __expf(x - m);
+        if (x != -INFINITY) {
+          const unsigned long long z = splitmix64(key + (unsigned long long)i);
+          const float u = ((float)(z >> 40) + 0.5f) * (1.0f / 16777216.0f);
+          const float gsc = x / o.temperature - logf(-logf(u));
+          if (better(gsc, i, bv, bi)) { bv = gsc; bi = i; bx = x; }
+        }
+      })
     } else {
-      for (int i = tid; i < V; i += LR_THREADS) {
-        const float xv = fval(i);
-        if (better(xv, i, bv, bi)) { bv = xv; bi = i; bx = xv; }
-      }
+      ROW_PASS(text_killed, {
+        se += __expf(x - m);
+        if (better(x, i, bv, bi)) { bv = x; bi = i; bx = x; }
+      })
     }
+    const float logS = logf(block_sum(se, sm));
     const int mine = bi;
     block_argbest(bv, bi, sm);
     // logprob of the chosen token: log_softmax(logits)[tok] (decoding.py:312-313)
@@ -201,29 +230,50 @@ __global__ __launch_bounds__(LR_THREADS) void k_logit_rows(float* __restrict__ l
     }
     return;
   }
-  // beam: top-(G+1) of the log-probabilities (value desc, index asc)
+  // beam: top-(G+1) of the log-probabilities (value desc, index asc).  The normaliser
+  // pass also takes each lane's maximum; the need-th largest of those maxima is a
+  // lower bound of the row's need-th largest value (need lanes hold an element at
+  // least that large), so the insertion pass only touches elements >= it — without
+  // the bound every wave would run the insertion chain on almost every element.
   const int need = s.G + 1;
+  float tmax = -INFINITY;
+  ROW_PASS(text_killed, {
+    se += __expf(x - m);
+    tmax = fmaxf(tmax, x);
+  })
+  float thr = -INFINITY;
+  {
+    float v = tmax;
+    for (int q = 0; q < need; ++q) {
+      float bv = v;
+      int bi = tid;
+      block_argbest(bv, bi, sm);
+      thr = bv;
+      if (bi == tid) v = -INFINITY;
+    }
+  }
   float lv[KC];
   int li[KC];
 #pragma unroll
   for (int q = 0; q < KC; ++q) { lv[q] = -INFINITY; li[q] = 0x7fffffff; }
   float thr_v = -INFINITY;  // the thread's current need-th best (entry to beat)
   int thr_i = 0x7fffffff;
-  for (int i = tid; i < V; i += LR_THREADS) {
-    float v = fval(i);
+  ROW_PASS(text_killed, {
+    float v = x;
     int vi = i;
-    if (!better(v, vi, thr_v, thr_i)) continue;
-#pragma unroll
-    for (int q = 0; q < KC; ++q) {
-      if (q < need && better(v, vi, lv[q], li[q])) {
-        const float tv = lv[q]; const int ti = li[q];
-        lv[q] = v; li[q] = vi; v = tv; vi = ti;
+    if (x >= thr && better(v, vi, thr_v, thr_i)) {
+      _Pragma("unroll") for (int q = 0; q < KC; ++q) {
+        if (q < need && better(v, vi, lv[q], li[q])) {
+          const float tv = lv[q]; const int ti = li[q];
+          lv[q] = v; li[q] = vi; v = tv; vi = ti;
+        }
       }
+      _Pragma("unroll") for (int q = 0; q < KC; ++q)
+        if (q == need - 1) { thr_v = lv[q]; thr_i = li[q]; }
     }
-#pragma unroll
-    for (int q = 0; q < KC; ++q)
-      if (q == need - 1) { thr_v = lv[q]; thr_i = li[q]; }
-  }
+  })
+#undef ROW_PASS
+  const float logS = logf(block_sum(se, sm));
   int head = 0;
   for (int q = 0; q < need; ++q) {
     float hv = -INFINITY;
@@ -288,26 +338,25 @@ __global__ __launch_bounds__(256) void k_merge(DecState s, DecOpts o) {
     if (p == len - 1 && p >= sb) a = b;  // this step's KV of beam b was written in slot b
     oa[b][p] = a;
   }
+  // candidates in insertion order: beam-major, top-k order (decoding.py:366-373);
+  // at the first update all beams are identical: dict keys collapse onto beam 0's
+  // candidates with the source of the last duplicate (G-1).  Gathered by one lane
+  // each (independent loads), then sorted by one lane from LDS.
+  __shared__ float csc[MG_MAXG * KC];
+  __shared__ int csrc[MG_MAXG * KC], ctok[MG_MAXG * KC];
+  const bool first = (len == sb);
+  const int nbeams = first ? 1 : G;
+  const int nc = nbeams * (G + 1);
+  if (tid < nc) {
+    const int b = tid / (G + 1), k = tid - b * (G + 1), r = w * G + b;
+    csc[tid] = s.sum_lp[r] + s.cand_val[r * KC + k];
+    ctok[tid] = s.cand_idx[r * KC + k];
+    csrc[tid] = first ? (G - 1) : b;
+  }
   __syncthreads();
   if (tid == 0) {
-    // candidates in insertion order: beam-major, top-k order (decoding.py:366-373);
-    // at the first update all beams are identical: dict keys collapse onto beam 0's
-    // candidates with the source of the last duplicate (G-1).
-    float csc[MG_MAXG * KC];
-    int csrc[MG_MAXG * KC], ctok[MG_MAXG * KC], order[MG_MAXG * KC];
-    int nc = 0;
-    const bool first = (len == sb);
-    const int nbeams = first ? 1 : G;
-    for (int b = 0; b < nbeams; ++b) {
-      const int r = w * G + b;
-      for (int k = 0; k < G + 1; ++k) {
-        csc[nc] = s.sum_lp[r] + s.cand_val[r * KC + k];
-        ctok[nc] = s.cand_idx[r * KC + k];
-        csrc[nc] = first ? (G - 1) : b;
-        order[nc] = nc;
-        ++nc;
-      }
-    }
+    int order[MG_MAXG * KC];
+    for (int c = 0; c < nc; ++c) order[c] = c;
     // stable sort by score desc (insertion sort keeps insertion order on ties)
     for (int i = 1; i < nc; ++i) {
       const int t = order[i];

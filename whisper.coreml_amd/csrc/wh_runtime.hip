@@ -1269,6 +1269,12 @@ struct Ctx : public wh_ctx {
       hipEventElapsedTime(&t, tm.a, tm.b);
       *ms = t / launches;
       return 0;
+    } else if (what == 4) {
+      // the token-selection kernel alone on the current logits (state unchanged)
+      if (cur_nwin < 1) return fail(-16, "no decode batch");
+      hipEventRecord(tm.a, st);
+      for (int i = 0; i < iters; ++i) launch_logit_rows(logits, V, S, O, cur_nwin, st);
+      hipEventRecord(tm.b, st);
     } else {
       return fail(-2, "time_stage: unknown stage");
     }
