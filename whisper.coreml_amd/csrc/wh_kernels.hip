@@ -1,6 +1,8 @@
 // Attention, LayerNorm, embedding and log-mel kernels for libwhisper_hip.
 #include "wh_kernels.h"
 
+#include <cstdlib>
+
 namespace wh {
 
 // ============================================================ LayerNorm
@@ -520,30 +522,30 @@ void launch_reduce_store(const float* part, int nsplit, int64_t part_stride, con
 }
 
 // ============================================================ decoder cross-attention (split-K flash decoding)
-// grid (windows, H, nsplit), block 256 = 4 waves; wave w of split sp owns the 64-key
-// tile sp*4 + w.  All rows of a window (its beams, or the prefill tokens) share the
+// grid (windows, H, nsplit), block 64*NW = NW waves; wave w of split sp owns the 64-key
+// tile sp*NW + w.  All rows of a window (its beams, or the prefill tokens) share the
 // pass, in row tiles of 16: K and V of a window are streamed from HBM once per step.
 // Both MFMA operands load straight from HBM into fragments: K in its natural
 // [key][64] layout (A of S^T = K Q^T), V stored transposed [64][Tk] at encode time
-// (A of O^T = V^T P^T), so no LDS staging is needed; LDS only combines the 4 waves.
+// (A of O^T = V^T P^T), so no LDS staging is needed; LDS only combines the NW waves.
 // ck: [win][head][TKP][64], cvt: [win][head][64][TKP] (key-permuted) for this layer.
 // Partials per split: po[row][h][split][64], pm/pl[row][h][split] (k_cross_combine).
 // If qk_map != null the raw scores q.k of alignment heads are also written
 // (word timestamps, decoder.py:306-308): qk_out[(qk_map[h] * qk_rows + row) * Tk + key].
-template <typename T>
-__global__ __launch_bounds__(256) void k_cross_attn(const T* __restrict__ q, int ldq, const T* __restrict__ ck,
+template <typename T, int NW>
+__global__ __launch_bounds__(64 * NW) void k_cross_attn(const T* __restrict__ q, int ldq, const T* __restrict__ ck,
                                                     const T* __restrict__ cvt, int Tk, int H, int nsplit,
                                                     const int* __restrict__ win_row0, const int* __restrict__ win_nrows,
                                                     const int* __restrict__ win_slot, int64_t win_stride,
                                                     float* __restrict__ po, float* __restrict__ pm, float* __restrict__ pl,
                                                     float* qk_out, const int* qk_map, int qk_rows) {
-  __shared__ float red_m[4][16], red_l[4][16];
-  __shared__ float red_o[4][64][17];
+  __shared__ float red_m[NW][16], red_l[NW][16];
+  __shared__ float red_o[NW][64][17];
   const int wi = blockIdx.x, h = blockIdx.y, sp = blockIdx.z;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int r = lane & 15, g = lane >> 4;
   const int row0 = win_row0[wi], nrows = win_nrows[wi];
-  const int kt0 = (sp * 4 + wave) * 64;
+  const int kt0 = (sp * NW + wave) * 64;
   const bool active = kt0 < Tk;
   const int qslot = qk_map ? qk_map[h] : -1;
   const T* kbase = ck + (int64_t)win_slot[wi] * win_stride + (int64_t)h * TKP * 64;
@@ -615,7 +617,7 @@ __global__ __launch_bounds__(256) void k_cross_attn(const T* __restrict__ q, int
 #pragma unroll
         for (int dt = 0; dt < 4; ++dt) mfma_step(acc[dt], vf[dt][s], pf[s]);
     }
-    // combine the 4 waves of this split (lanes of every g hold the row stats of q = r)
+    // combine the NW waves of this split (lanes of every g hold the row stats of q = r)
     if (g == 0) {
       red_m[wave][r] = m;
       red_l[wave][r] = l;
@@ -625,14 +627,14 @@ __global__ __launch_bounds__(256) void k_cross_attn(const T* __restrict__ q, int
 #pragma unroll
       for (int j = 0; j < 4; ++j) red_o[wave][dt * 16 + 4 * g + j][r] = acc[dt][j];
     __syncthreads();
-    {
+    if (tid < 256) {
       const int qq = tid >> 4, dc = (tid & 15) * 4;  // 16 rows x 16 chunks of 4 dims
       float M = -INFINITY;
 #pragma unroll
-      for (int w = 0; w < 4; ++w) M = fmaxf(M, red_m[w][qq]);
-      float f[4], L = 0.f;
+      for (int w = 0; w < NW; ++w) M = fmaxf(M, red_m[w][qq]);
+      float f[NW], L = 0.f;
 #pragma unroll
-      for (int w = 0; w < 4; ++w) {
+      for (int w = 0; w < NW; ++w) {
         f[w] = red_m[w][qq] == -INFINITY ? 0.f : exp2f((red_m[w][qq] - M) * LOG2E);
         L += f[w] * red_l[w][qq];
       }
@@ -644,7 +646,7 @@ __global__ __launch_bounds__(256) void k_cross_attn(const T* __restrict__ q, int
         for (int e = 0; e < 4; ++e) {
           o[e] = 0.f;
 #pragma unroll
-          for (int w = 0; w < 4; ++w) o[e] += f[w] * red_o[w][dc + e][qq];
+          for (int w = 0; w < NW; ++w) o[e] += f[w] * red_o[w][dc + e][qq];
         }
         store4(po + pi * 64 + dc, o[0], o[1], o[2], o[3]);
         if (dc == 0) {
@@ -680,9 +682,20 @@ void launch_cross_attn(const T* q, int ldq, const T* ck, const T* cv, int Tk, in
                        float* pm, float* pl, T* out, int ldo, int rows, float* qk_out, const int* qk_map, int qk_rows,
                        hipStream_t st) {
   if (rows <= 0) return;
-  nsplit = ((Tk + 63) / 64 + 3) / 4;  // one 64-key tile per wave, 4 waves per split
-  k_cross_attn<T><<<dim3(nwin, H, nsplit), 256, 0, st>>>(q, ldq, ck, cv, Tk, H, nsplit, win_row0, win_nrows, win_slot,
-                                                         win_stride, po, pm, pl, qk_out, qk_map, qk_rows);
+  // one 64-key tile per wave, 8 waves per split (3 splits at Tk = 1500: half the
+  // partials of 4-wave splits, -75 us per 20-window beam step);
+  // WHISPER_HIP_XATTN_WAVES=4 selects 4-wave splits
+  static const int nw = [] {
+    const char* e = getenv("WHISPER_HIP_XATTN_WAVES");
+    return e && atoi(e) == 4 ? 4 : 8;
+  }();
+  nsplit = ((Tk + 63) / 64 + nw - 1) / nw;
+  if (nw == 8)
+    k_cross_attn<T, 8><<<dim3(nwin, H, nsplit), 512, 0, st>>>(q, ldq, ck, cv, Tk, H, nsplit, win_row0, win_nrows,
+                                                              win_slot, win_stride, po, pm, pl, qk_out, qk_map, qk_rows);
+  else
+    k_cross_attn<T, 4><<<dim3(nwin, H, nsplit), 256, 0, st>>>(q, ldq, ck, cv, Tk, H, nsplit, win_row0, win_nrows,
+                                                              win_slot, win_stride, po, pm, pl, qk_out, qk_map, qk_rows);
   k_cross_combine<T><<<dim3(rows, H), 64, 0, st>>>(po, pm, pl, H, nsplit, out, ldo);
 }
 

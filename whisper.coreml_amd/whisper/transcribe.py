@@ -22,7 +22,6 @@ The log-mel of the whole file is computed on the GPU and stays there; windows
 are cut from it on the device.
 """
 
-import copy
 import os
 import warnings
 from dataclasses import replace
@@ -33,7 +32,7 @@ import numpy as np
 from .audio import FRAMES_PER_SECOND, HOP_LENGTH, N_FRAMES, N_SAMPLES, SAMPLE_RATE, load_audio
 from .backend_hip import DeviceAudio
 from .decoding import DecodingOptions, DecodingResult, detect_language, run_windows
-from .timing import apply_alignment, find_alignment, find_alignment_batch
+from .timing import WordTiming, apply_alignment, find_alignment, find_alignment_batch
 from .tokenizer import LANGUAGES, get_tokenizer
 
 if TYPE_CHECKING:
@@ -318,7 +317,8 @@ def _window_alignment(model, st, segs: List[dict], segment_size: int, slot: int)
 def _words_and_seek(st, segs, alignment, seek, previous_seek, segment_size, single_end, last_speech):
     """transcribe.py:412-426 on a precomputed alignment: words of every segment, the
     seek refinement from the last word; returns (seek, last_speech_timestamp)."""
-    apply_alignment(segs, copy.deepcopy(alignment), st["tokenizer"], st["prepend"], st["append"], last_speech)
+    fresh = [WordTiming(w.word, list(w.tokens), w.start, w.end, w.probability) for w in alignment]
+    apply_alignment(segs, fresh, st["tokenizer"], st["prepend"], st["append"], last_speech)
     time_offset = float(previous_seek * HOP_LENGTH / SAMPLE_RATE)
     if not single_end:
         last_word_end = get_end(segs)
