@@ -42,6 +42,7 @@ def parse():
     p.add_argument("--max-windows", type=int, default=20)
     p.add_argument("--cpu-baseline", type=int, default=1)
     p.add_argument("--cpu-steps", type=int, default=6, help="decoder steps in the CPU baseline sample")
+    p.add_argument("--dump", default="", help="write the last step's segments (tokens, avg_logprob) as JSON")
     p.add_argument("--word-timestamps", type=int, default=0,
                    help="config 5: transcribe(word_timestamps=True) (alignment + DTW on the GPU per window)")
     return p.parse_args()
@@ -212,6 +213,11 @@ def main():
     elapsed = time.perf_counter() - t0
     st1 = model.ctx.stats()
     elapsed_max = allreduce_max(pg, elapsed)
+
+    if args.dump and rank == 0:
+        with open(args.dump, "w") as f:
+            json.dump([{k: s[k] for k in ("seek", "tokens", "avg_logprob", "no_speech_prob")}
+                       for s in results[-1]["segments"]], f)
 
     # segment gather to rank 0 (the only data-path exchange besides the mel max)
     seg_tokens = sum(len(s["tokens"]) for s in results[-1]["segments"])

@@ -223,16 +223,18 @@ __global__ __launch_bounds__(512) void k_gemv_rows(GemmArgs a) {
 // flight before the first MFMA).  grid: (ceil(N/64), ceil(M/(16*MT)), ksplit).
 constexpr int XS_BYTES = 512;              // bytes of K per LDS subchunk row
 constexpr int XS_ROW = XS_BYTES + 16;      // padded row: conflict-free ds_read_b128
-template <typename T, int MT, int EPI>
-__global__ __launch_bounds__(256) void k_gemv_x(GemmArgs a) {
+template <typename T, int MT, int EPI, int NW = 4>
+__global__ __launch_bounds__(64 * NW) void k_gemv_x(GemmArgs a) {
+  constexpr int NT = 64 * NW;
   constexpr int KCH = XS_BYTES / (int)sizeof(T);  // k per subchunk (256 half / 128 float)
   constexpr int KS = KCH / 32;                    // k-steps per subchunk
   constexpr int CPR = XS_BYTES / 16;              // 16 B chunks per staged row (32)
-  constexpr int NCH = (MT * 16 * CPR) / 256;      // chunks per thread (= 2 MT)
+  constexpr int NCH = (MT * 16 * CPR + NT - 1) / NT;  // chunks per thread
+  constexpr bool RAG = (MT * 16 * CPR) % NT != 0;
   __shared__ __attribute__((aligned(16))) char xs[MT * 16 * XS_ROW];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int r = lane & 15, g = lane >> 4;
-  const int n0 = blockIdx.x * 64 + wave * 16;
+  const int n0 = blockIdx.x * 16 * NW + wave * 16;
   const int mb = blockIdx.y * (16 * MT);
   const int kz = blockIdx.z;
   const int S = a.K / 32;
@@ -247,7 +249,7 @@ __global__ __launch_bounds__(256) void k_gemv_x(GemmArgs a) {
   const char* xsrc[NCH];
 #pragma unroll
   for (int i = 0; i < NCH; ++i) {
-    const int c = tid + 256 * i, row = c / CPR;
+    const int c = tid + NT * i, row = min(c / CPR, MT * 16 - 1);
     int m = mb + row;
     if (m >= a.M) m = a.M - 1;
     const int xr = a.x_rows ? a.x_rows[m] : m;
@@ -266,7 +268,7 @@ __global__ __launch_bounds__(256) void k_gemv_x(GemmArgs a) {
     for (int s = 0; s < KS; ++s) frag_load(w[s], wp + kc + min(s, ns - 1) * 32);
 #pragma unroll
     for (int i = 0; i < NCH; ++i) {
-      const int ch = (tid + 256 * i) % CPR;
+      const int ch = (tid + NT * i) % CPR;
       xr[i] = *reinterpret_cast<const float4_t*>(xsrc[i] + (int64_t)kc * sizeof(T) + (min(ch, cpr - 1) - ch) * 16);
     }
   };
@@ -275,8 +277,8 @@ __global__ __launch_bounds__(256) void k_gemv_x(GemmArgs a) {
     const int ns = min(KCH, Kc - kc) / 32;
 #pragma unroll
     for (int i = 0; i < NCH; ++i) {
-      const int c = tid + 256 * i;
-      *reinterpret_cast<float4_t*>(xs + (c / CPR) * XS_ROW + (c % CPR) * 16) = xr[i];
+      const int c = tid + NT * i;
+      if (!RAG || c < MT * 16 * CPR) *reinterpret_cast<float4_t*>(xs + (c / CPR) * XS_ROW + (c % CPR) * 16) = xr[i];
     }
     __syncthreads();
     const bool more = kc + KCH < Kc;
@@ -366,6 +368,31 @@ int launch_gemm(const GemmArgs& a, int epi, hipStream_t st) {
     const int rows_per = rows_per_block(a.M, a.mt_block);
     const int ks = epi == EPI_PARTIAL ? a.ksplit : 1;
     if (ks < 1 || ks > a.K / 32) return -4;
+    if (mt >= 3 && epi == EPI_F32_COLS && a.N >= 16384) {
+      // vocabulary projection: NW column tiles share each staged X subchunk, so X
+      // (re-read from L2 by every workgroup) costs 112/(16 NW) of the weight bytes
+      static const int nw = [] {
+        const char* e = getenv("WHISPER_HIP_VOCAB_WAVES");
+        const int v = e ? atoi(e) : 8;
+        return v == 4 ? 4 : 8;  // 16 waves spill
+      }();
+      dim3 gv((a.N + 16 * nw - 1) / (16 * nw), (a.M + 16 * rows_per - 1) / (16 * rows_per), 1);
+#define LAUNCHV(MT_)                                                                                  \
+  switch (nw) {                                                                                      \
+    case 4: k_gemv_x<T, MT_, EPI_F32_COLS, 4><<<gv, 256, 0, st>>>(a); break;                         \
+    default: k_gemv_x<T, MT_, EPI_F32_COLS, 8><<<gv, 512, 0, st>>>(a); break;                        \
+  }
+      switch (rows_per) {
+        case 3: LAUNCHV(3) break;
+        case 4: LAUNCHV(4) break;
+        case 5: LAUNCHV(5) break;
+        case 6: LAUNCHV(6) break;
+        case 7: LAUNCHV(7) break;
+        default: LAUNCHV(8) break;
+      }
+#undef LAUNCHV
+      return 0;
+    }
     if (mt >= 3 && (epi == EPI_PARTIAL || (a.N + 63) / 64 >= 70)) {  // tall-skinny: X shared via LDS by 4 column tiles
       dim3 gx((a.N + 63) / 64, (a.M + 16 * rows_per - 1) / (16 * rows_per), ks);
 #define LAUNCHX(MT_)                                                                            \

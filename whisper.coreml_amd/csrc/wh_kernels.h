@@ -26,11 +26,21 @@ void launch_self_attn_qkv(const float* part, int nsplit, int64_t part_stride, co
 template <typename T>
 void launch_reduce_store(const float* part, int nsplit, int64_t part_stride, const float* bias, T* out, int ldo, int M,
                          int N, int gelu, hipStream_t st);
+// decoder-step query given as split-K slabs: q = bias + sum_z part[z*stride + row*ldq + c]
+// (part == nullptr: q is a T matrix); needs <= 16 rows per window and z in {4, 8}
+// (cross_attn_q_slabs(z)).
+struct XQPart {
+  const float* part = nullptr;
+  int64_t stride = 0;
+  int z = 0;
+  const float* bias = nullptr;
+};
+inline bool cross_attn_q_slabs(int z) { return z == 4 || z == 8; }
 template <typename T>
 void launch_cross_attn(const T* q, int ldq, const T* ck, const T* cv, int Tk, int H, int nsplit, int nwin,
                        const int* win_row0, const int* win_nrows, const int* win_slot, int64_t win_stride, float* po,
                        float* pm, float* pl, T* out, int ldo, int rows, float* qk_out, const int* qk_map, int qk_rows,
-                       hipStream_t st);
+                       hipStream_t st, XQPart xq = XQPart());
 template <typename T>
 void launch_embed(const T* E, const T* P, int n, const int* row_tok, int* row_pos, const int* hist,
                   const int* cur_len, int G, int hctx, int pmax, float* x, int rows, hipStream_t st);

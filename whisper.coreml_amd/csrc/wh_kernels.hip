@@ -532,15 +532,17 @@ void launch_reduce_store(const float* part, int nsplit, int64_t part_stride, con
 // Partials per split: po[row][h][split][64], pm/pl[row][h][split] (k_cross_combine).
 // If qk_map != null the raw scores q.k of alignment heads are also written
 // (word timestamps, decoder.py:306-308): qk_out[(qk_map[h] * qk_rows + row) * Tk + key].
-template <typename T, int NW>
-__global__ __launch_bounds__(64 * NW) void k_cross_attn(const T* __restrict__ q, int ldq, const T* __restrict__ ck,
-                                                    const T* __restrict__ cvt, int Tk, int H, int nsplit,
+template <typename T, int NW, int QZ>
+__global__ __launch_bounds__(64 * NW) void k_cross_attn(const T* __restrict__ q, int ldq, const T* ck,
+                                                    const T* cvt, int Tk, int H, int nsplit,
                                                     const int* __restrict__ win_row0, const int* __restrict__ win_nrows,
                                                     const int* __restrict__ win_slot, int64_t win_stride,
                                                     float* __restrict__ po, float* __restrict__ pm, float* __restrict__ pl,
-                                                    float* qk_out, const int* qk_map, int qk_rows) {
+                                                    float* qk_out, const int* qk_map, int qk_rows, XQPart xq) {
   __shared__ float red_m[NW][16], red_l[NW][16];
   __shared__ float red_o[NW][64][17];
+  constexpr bool QP = QZ > 0;
+  __shared__ __attribute__((aligned(16))) T qs[QP ? 32 : 1][72];  // rows 16..31: waves 4..7's dummy copies
   const int wi = blockIdx.x, h = blockIdx.y, sp = blockIdx.z;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int r = lane & 15, g = lane >> 4;
@@ -552,19 +554,42 @@ __global__ __launch_bounds__(64 * NW) void k_cross_attn(const T* __restrict__ q,
   const T* vbase = cvt + (int64_t)win_slot[wi] * win_stride + (int64_t)h * 64 * TKP;
   constexpr float LOG2E = 1.4426950408889634f;
   // K and V fragments of this wave's tile do not depend on the rows: load them once,
-  // all in flight together (V^T is key-permuted so each lane's 8 keys are contiguous)
+  // all in flight together (V^T is key-permuted so each lane's 8 keys are contiguous).
+  // QP (decoder step, <= 16 rows per window): q = bias + sum of the projection's
+  // split-K slabs (k_reduce_store's order), reduced here into LDS instead of by a
+  // separate launch; its loads go between K's and V's, so the wait for them leaves
+  // V in flight (the first MFMAs need K and q, not V)
+  // (no branch around any of these loads: a branch makes the compiler's wait for q
+  // a full drain; an inactive wave loads tile 0 and skips its MFMAs)
+  const int ktl = active ? kt0 : 0;
   Frag<T> kf[4][2], vf[4][2];
-  if (active) {
 #pragma unroll
-    for (int kt = 0; kt < 4; ++kt) {
-      const T* kp = kbase + (int64_t)(kt0 + kt * 16 + r) * 64 + 8 * g;
-      frag_load(kf[kt][0], kp);
-      frag_load(kf[kt][1], kp + 32);
-    }
+  for (int kt = 0; kt < 4; ++kt) {
+    const T* kp = kbase + (int64_t)(ktl + kt * 16 + r) * 64 + 8 * g;
+    frag_load(kf[kt][0], kp);
+    frag_load(kf[kt][1], kp + 32);
+  }
+  float4_t qv = (float4_t){0.f, 0.f, 0.f, 0.f}, pp[QP ? QZ : 1];
+  __builtin_amdgcn_sched_barrier(0);  // keep the load groups in K, q, V order
+  if constexpr (QP) {
+    // waves 4..7 repeat waves 0..3's loads (L1 hits) to stay branch-free; the slab
+    // count is a template constant so no load is sunk into a conditional
+    const int t = tid & 255, qq = min(t >> 4, nrows - 1), c = h * 64 + (t & 15) * 4;
+    const float* src = xq.part + (int64_t)(row0 + qq) * ldq + c;
 #pragma unroll
-    for (int dt = 0; dt < 4; ++dt)
+    for (int z = 0; z < QZ; ++z) pp[z] = load4f(src + z * xq.stride);
+    qv = load4f(xq.bias + c);
+  }
+  __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-      for (int s = 0; s < 2; ++s) frag_load(vf[dt][s], vbase + (int64_t)(dt * 16 + r) * TKP + kt0 + 32 * s + 8 * g);
+  for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+    for (int s = 0; s < 2; ++s) frag_load(vf[dt][s], vbase + (int64_t)(dt * 16 + r) * TKP + ktl + 32 * s + 8 * g);
+  if constexpr (QP) {
+#pragma unroll
+    for (int z = 0; z < QZ; ++z) qv += pp[z];
+    store4(&qs[tid >> 4][(tid & 15) * 4], qv[0], qv[1], qv[2], qv[3]);  // unconditional: no load is sunk
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // LDS only: V stays in flight
   }
   for (int rt = 0; rt < nrows; rt += 16) {
     int qr = rt + r;
@@ -576,9 +601,14 @@ __global__ __launch_bounds__(64 * NW) void k_cross_attn(const T* __restrict__ q,
     for (int i = 0; i < 4; ++i) acc[i] = (float4_t){0.f, 0.f, 0.f, 0.f};
     if (active) {
       Frag<T> qf[2];
-      const T* qp = q + (int64_t)(row0 + qr) * ldq + h * 64 + 8 * g;
-      frag_load(qf[0], qp);
-      frag_load(qf[1], qp + 32);
+      if constexpr (QP) {
+        frag_load(qf[0], &qs[qr][8 * g]);
+        frag_load(qf[1], &qs[qr][32 + 8 * g]);
+      } else {
+        const T* qp = q + (int64_t)(row0 + qr) * ldq + h * 64 + 8 * g;
+        frag_load(qf[0], qp);
+        frag_load(qf[1], qp + 32);
+      }
       float4_t sc[4];
 #pragma unroll
       for (int kt = 0; kt < 4; ++kt) {
@@ -680,22 +710,22 @@ template <typename T>
 void launch_cross_attn(const T* q, int ldq, const T* ck, const T* cv, int Tk, int H, int nsplit, int nwin,
                        const int* win_row0, const int* win_nrows, const int* win_slot, int64_t win_stride, float* po,
                        float* pm, float* pl, T* out, int ldo, int rows, float* qk_out, const int* qk_map, int qk_rows,
-                       hipStream_t st) {
+                       hipStream_t st, XQPart xq) {
   if (rows <= 0) return;
   // one 64-key tile per wave, 8 waves per split (3 splits at Tk = 1500: half the
-  // partials of 4-wave splits, -75 us per 20-window beam step);
-  // WHISPER_HIP_XATTN_WAVES=4 selects 4-wave splits
-  static const int nw = [] {
-    const char* e = getenv("WHISPER_HIP_XATTN_WAVES");
-    return e && atoi(e) == 4 ? 4 : 8;
-  }();
-  nsplit = ((Tk + 63) / 64 + nw - 1) / nw;
-  if (nw == 8)
-    k_cross_attn<T, 8><<<dim3(nwin, H, nsplit), 512, 0, st>>>(q, ldq, ck, cv, Tk, H, nsplit, win_row0, win_nrows,
-                                                              win_slot, win_stride, po, pm, pl, qk_out, qk_map, qk_rows);
-  else
-    k_cross_attn<T, 4><<<dim3(nwin, H, nsplit), 256, 0, st>>>(q, ldq, ck, cv, Tk, H, nsplit, win_row0, win_nrows,
-                                                              win_slot, win_stride, po, pm, pl, qk_out, qk_map, qk_rows);
+  // partials of 4-wave splits, -75 us per 20-window beam step)
+  constexpr int NW = 8;
+  nsplit = ((Tk + 63) / 64 + NW - 1) / NW;
+  const dim3 grid(nwin, H, nsplit);
+#define XA(QZ_)                                                                                          \
+  k_cross_attn<T, NW, QZ_><<<grid, 64 * NW, 0, st>>>(q, ldq, ck, cv, Tk, H, nsplit, win_row0, win_nrows, win_slot, \
+                                                     win_stride, po, pm, pl, qk_out, qk_map, qk_rows, xq)
+  switch (xq.part ? xq.z : 0) {
+    case 4: XA(4); break;
+    case 8: XA(8); break;
+    default: XA(0); break;
+  }
+#undef XA
   k_cross_combine<T><<<dim3(rows, H), 64, 0, st>>>(po, pm, pl, H, nsplit, out, ldo);
 }
 
@@ -876,7 +906,7 @@ void launch_mel_norm(float* mel, int64_t count, int64_t ld, int n_mels, const un
                                     const int*, int, int, int, int, T*, int, int, hipStream_t);                          \
   template void launch_cross_attn<T>(const T*, int, const T*, const T*, int, int, int, int, const int*, const int*, \
                                      const int*, int64_t, float*, float*, float*, T*, int, int, float*,             \
-                                     const int*, int, hipStream_t);                                                         \
+                                     const int*, int, hipStream_t, XQPart);                                                 \
   template void launch_embed<T>(const T*, const T*, int, const int*, int*, const int*, const int*, int, int, int,  \
                                 float*, int, hipStream_t);                                                          \
   template void launch_mel_windows<T>(const float*, int64_t, int, const int64_t*, const int*, T*, int64_t, int, int, \

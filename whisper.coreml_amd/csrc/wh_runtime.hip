@@ -193,6 +193,7 @@ struct Ctx : public wh_ctx {
     if (d_audio) hipFree(d_audio);
     if (d_mel) hipFree(d_mel);
     for (auto& kv : d_filters) hipFree(kv.second);
+    if (d_gmax) hipFree(d_gmax);
     if (h_done) hipHostFree(h_done);
   }
 
@@ -736,11 +737,24 @@ struct Ctx : public wh_ctx {
         launch_self_attn<T>(q_d, n, kc[l], vc[l], rw, rs, rp, S.anc, ancG, Gcap, nh, CTX, att_d, n, R, st);
       }
       TRY(resid(att_d, n, e.wo, e.bo, R, e.lnx_g, e.lnx_b));
-      TRY(proj(e.wqx, e.bqx, R, n, q_d, 0, skinny));
+      // cross-attention query: in step mode its split-K slabs are reduced inside
+      // k_cross_attn (rows per window <= Gcap <= 8), otherwise projected directly
+      XQPart xq;
+      if (skinny && xq_fused) {
+        int ks = 0;
+        TRY(partial(xn_d, n, e.wqx, R, n, n, &ks));
+        if (cross_attn_q_slabs(ks)) {
+          xq.part = part; xq.stride = (int64_t)R * n; xq.z = ks; xq.bias = e.bqx;
+        } else {
+          launch_reduce_store<T>(part, ks, (int64_t)R * n, e.bqx, q_d, n, R, n, 0, st);
+        }
+      } else {
+        TRY(proj(e.wqx, e.bqx, R, n, q_d, 0, skinny));
+      }
       const T* ck = ckv + (size_t)(2 * l) * Wcap * TKP * n;
       const T* cv = ckv + (size_t)(2 * l + 1) * Wcap * TKP * n;
       launch_cross_attn<T>(q_d, n, ck, cv, 1500, nh, NSPLIT, nwin, wr0, wnr, wsl, (int64_t)TKP * n, po, pm, pl, att_d,
-                           n, R, aqk, qkmap ? qkmap + l * nh : nullptr, qkrows, st);
+                           n, R, aqk, qkmap ? qkmap + l * nh : nullptr, qkrows, st, xq);
       TRY(resid(att_d, n, e.wox, e.box, R, e.ln2_g, e.ln2_b));
       TRY(proj(e.w1, e.b1, R, 4 * n, hm_d, 1, skinny));
       const bool last = l + 1 == Ld;
@@ -932,6 +946,12 @@ struct Ctx : public wh_ctx {
     graph_key = key;
     return 0;
   }
+
+  // WHISPER_HIP_XQ=0 keeps the separate cross-query reduce (A/B switch)
+  const bool xq_fused = [] {
+    const char* e = getenv("WHISPER_HIP_XQ");
+    return !(e && e[0] == '0');
+  }();
 
   // WHISPER_HIP_EAGER=1 launches the step kernels directly instead of replaying the
   // captured graph (same kernels; used under profilers that do not follow graphs)

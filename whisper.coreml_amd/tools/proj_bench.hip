@@ -2,7 +2,7 @@
 // split-K k_gemv_x + fixed-order reduce pair, per projection shape of a large-v3
 // decoder layer.  Every timing averages over 32 distinct weight copies so weights
 // stream from HBM as in a 32-layer step (not from the 256 MB Infinity Cache).
-//   make -C whisper.coreml_amd tools/proj_bench && ./whisper.coreml_amd/tools/proj_bench [rows]
+//   make -C whisper.coreml_amd tools/proj_bench && ./whisper.coreml_amd/tools/proj_bench [rows [copies]]
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
@@ -59,7 +59,8 @@ static const Var VARS[] = {V18(4), V18(7), V3(2, 4, 1), V3(2, 4, 2)};
 
 int main(int argc, char** argv) {
   const int M = argc > 1 ? atoi(argv[1]) : 100;
-  const int n = 1280, L = 32, iters = 4;
+  // argv[2] = distinct weight copies (32: HBM-cold as in a step; 1: Infinity-Cache warm)
+  const int n = 1280, L = argc > 2 ? atoi(argv[2]) : 32, iters = 128 / L;
   struct Shape { const char* name; int N, K; };
   const Shape shapes[] = {{"qkv", 3 * n, n}, {"out", n, n}, {"fc1", 4 * n, n}, {"fc2", n, 4 * n}};
   const size_t wsz = (size_t)4 * n * n;
