@@ -27,15 +27,16 @@ template <typename T>
 void launch_reduce_store(const float* part, int nsplit, int64_t part_stride, const float* bias, T* out, int ldo, int M,
                          int N, int gelu, hipStream_t st);
 // decoder-step query given as split-K slabs: q = bias + sum_z part[z*stride + row*ldq + c]
-// (part == nullptr: q is a T matrix); needs <= 16 rows per window and z in {4, 8}
+// (part == nullptr: q is a T matrix); needs <= 16 rows per window and z in {4, 8, 10}
 // (cross_attn_q_slabs(z)).
 struct XQPart {
   const float* part = nullptr;
   int64_t stride = 0;
   int z = 0;
   const float* bias = nullptr;
+  int max_rows = 0;  // rows per window when known (decoder step: the beam group)
 };
-inline bool cross_attn_q_slabs(int z) { return z == 4 || z == 8; }
+inline bool cross_attn_q_slabs(int z) { return z == 4 || z == 8 || z == 10; }
 template <typename T>
 void launch_cross_attn(const T* q, int ldq, const T* ck, const T* cv, int Tk, int H, int nsplit, int nwin,
                        const int* win_row0, const int* win_nrows, const int* win_slot, int64_t win_stride, float* po,

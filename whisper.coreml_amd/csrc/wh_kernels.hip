@@ -706,12 +706,205 @@ __global__ __launch_bounds__(64) void k_cross_combine(const float* __restrict__ 
   out[(int64_t)row * ldo + h * 64 + lane] = from_f32<T>(num / den);
 }
 
+// Decoder-step variant: ONE workgroup per (window, head) covers all keys, so there is
+// no split partial and no k_cross_combine launch.  8 waves; wave w takes tiles
+// w, w+8, w+16, ... (TPW per wave, compile-time) with an online softmax, the next
+// tile's K/V fragments in flight while the current tile is computed; the 8 waves'
+// (m, l, O) are merged in LDS and the normalised rows written as T.  <= 16 rows per
+// window (beams of a step), query from q or reduced from split-K slabs (QZ > 0).
+template <typename T, int QZ, int TPW, bool PF>
+__global__ __launch_bounds__(512, PF ? 1 : 2) void k_cross_attn1(const T* __restrict__ q, int ldq, const T* ck, const T* cvt,
+                                                     int Tk, const int* __restrict__ win_row0,
+                                                     const int* __restrict__ win_nrows, const int* __restrict__ win_slot,
+                                                     int64_t win_stride, XQPart xq, T* __restrict__ out, int ldo) {
+  constexpr int NW = 8;
+  constexpr bool QP = QZ > 0;
+  constexpr float LOG2E = 1.4426950408889634f;
+  __shared__ float red_m[NW][16], red_l[NW][16];
+  __shared__ float red_o[NW][64][17];
+  __shared__ __attribute__((aligned(16))) T qs[32][72];
+  const int wi = blockIdx.x, h = blockIdx.y, H = gridDim.y;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int r = lane & 15, g = lane >> 4;
+  const int row0 = win_row0[wi], nrows = win_nrows[wi];
+  const int ntiles = (Tk + 63) / 64;
+  const T* kbase = ck + (int64_t)win_slot[wi] * win_stride + (int64_t)h * TKP * 64;
+  const T* vbase = cvt + (int64_t)win_slot[wi] * win_stride + (int64_t)h * 64 * TKP;
+  // loads are never branched around (a branch turns the compiler's counted waits into
+  // full drains): tiles past the end reload the wave's first tile and skip the math
+  auto load_kv = [&](int it, Frag<T> (&kf)[4][2], Frag<T> (&vf)[4][2]) {
+    const int t = wave + NW * it, kt0 = (t < ntiles ? t : wave) * 64;
+#pragma unroll
+    for (int kt = 0; kt < 4; ++kt) {
+      const T* kp = kbase + (int64_t)(kt0 + kt * 16 + r) * 64 + 8 * g;
+      frag_load(kf[kt][0], kp);
+      frag_load(kf[kt][1], kp + 32);
+    }
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+      for (int s = 0; s < 2; ++s) frag_load(vf[dt][s], vbase + (int64_t)(dt * 16 + r) * TKP + kt0 + 32 * s + 8 * g);
+  };
+  // PF: the next tile's fragments load while this tile computes (2 register sets,
+  // one workgroup per CU); !PF: one set, two workgroups per CU hide each other
+  Frag<T> kf[PF ? 2 : 1][4][2], vf[PF ? 2 : 1][4][2];
+  load_kv(0, kf[0], vf[0]);
+  // the query rows -> LDS
+  float4_t qv = (float4_t){0.f, 0.f, 0.f, 0.f};
+  {
+    const int t = tid & 255, qq = min(t >> 4, nrows - 1), c = h * 64 + (t & 15) * 4;
+    if constexpr (QP) {
+      float4_t pp[QP ? QZ : 1];
+      const float* src = xq.part + (int64_t)(row0 + qq) * ldq + c;
+#pragma unroll
+      for (int z = 0; z < QZ; ++z) pp[z] = load4f(src + z * xq.stride);
+      qv = load4f(xq.bias + c);
+#pragma unroll
+      for (int z = 0; z < QZ; ++z) qv += pp[z];
+    } else {
+      const T* src = q + (int64_t)(row0 + qq) * ldq + c;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) qv[e] = (float)src[e];
+    }
+  }
+  store4(&qs[tid >> 4][(tid & 15) * 4], qv[0], qv[1], qv[2], qv[3]);
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // LDS only: K/V stay in flight
+  const int qr = min(r, nrows - 1);
+  Frag<T> qf[2];
+  frag_load(qf[0], &qs[qr][8 * g]);
+  frag_load(qf[1], &qs[qr][32 + 8 * g]);
+
+  float m = -INFINITY, l = 0.f;
+  float4_t acc[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) acc[i] = (float4_t){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int it = 0; it < TPW; ++it) {
+    const int cur = PF ? (it & 1) : 0;
+    if constexpr (PF) {
+      if (it + 1 < TPW) load_kv(it + 1, kf[cur ^ 1], vf[cur ^ 1]);
+    } else {
+      if (it > 0) load_kv(it, kf[0], vf[0]);
+    }
+    const int t = wave + NW * it;
+    if (t < ntiles) {
+      const int kt0 = t * 64;
+      float4_t sc[4];
+#pragma unroll
+      for (int kt = 0; kt < 4; ++kt) {
+        sc[kt] = (float4_t){0.f, 0.f, 0.f, 0.f};
+        mfma_step(sc[kt], kf[cur][kt][0], qf[0]);
+        mfma_step(sc[kt], kf[cur][kt][1], qf[1]);
+      }
+      float mx = -INFINITY;
+#pragma unroll
+      for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          if (kt0 + kt * 16 + 4 * g + j >= Tk) sc[kt][j] = -INFINITY;
+          mx = fmaxf(mx, sc[kt][j]);
+        }
+      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      const float mn = fmaxf(m, mx);
+      const float sf = m == -INFINITY ? 0.f : exp2f((m - mn) * LOG2E);
+      m = mn;
+      Frag<T> pf[2];
+      float ps = 0.f;
+#pragma unroll
+      for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const float p = exp2f((sc[kt][j] - m) * LOG2E);
+          ps += p;
+          pf[kt >> 1].v[(kt & 1) * 4 + j] = from_f32<T>(p);
+        }
+      ps += __shfl_xor(ps, 16, 64);
+      ps += __shfl_xor(ps, 32, 64);
+      l = l * sf + ps;
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) acc[dt] *= sf;
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt) mfma_step(acc[dt], vf[cur][dt][s], pf[s]);
+    }
+  }
+  // merge the 8 waves (lanes of every g hold the row stats of q = r)
+  if (g == 0) {
+    red_m[wave][r] = m;
+    red_l[wave][r] = l;
+  }
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) red_o[wave][dt * 16 + 4 * g + j][r] = acc[dt][j];
+  __syncthreads();
+  if (tid < 256) {
+    const int qq = tid >> 4, dc = (tid & 15) * 4;
+    if (qq < nrows) {
+      float M = -INFINITY;
+#pragma unroll
+      for (int w = 0; w < NW; ++w) M = fmaxf(M, red_m[w][qq]);
+      float f[NW], L = 0.f;
+#pragma unroll
+      for (int w = 0; w < NW; ++w) {
+        f[w] = red_m[w][qq] == -INFINITY ? 0.f : exp2f((red_m[w][qq] - M) * LOG2E);
+        L += f[w] * red_l[w][qq];
+      }
+      const float inv = 1.f / L;
+      float o[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        o[e] = 0.f;
+#pragma unroll
+        for (int w = 0; w < NW; ++w) o[e] += f[w] * red_o[w][dc + e][qq];
+        o[e] *= inv;
+      }
+      store4(out + (int64_t)(row0 + qq) * ldo + h * 64 + dc, o[0], o[1], o[2], o[3]);
+    }
+  }
+}
+
 template <typename T>
 void launch_cross_attn(const T* q, int ldq, const T* ck, const T* cv, int Tk, int H, int nsplit, int nwin,
                        const int* win_row0, const int* win_nrows, const int* win_slot, int64_t win_stride, float* po,
                        float* pm, float* pl, T* out, int ldo, int rows, float* qk_out, const int* qk_map, int qk_rows,
                        hipStream_t st, XQPart xq) {
   if (rows <= 0) return;
+  static const bool one = [] {
+    const char* e = getenv("WHISPER_HIP_XATTN1");
+    return !(e && e[0] == '0');
+  }();
+  static const bool pf = [] {
+    const char* e = getenv("WHISPER_HIP_XATTN1_PF");
+    return !(e && e[0] == '0');
+  }();
+  const int ntiles = (Tk + 63) / 64, tpw = (ntiles + 7) / 8;
+  if (one && xq.max_rows >= 1 && xq.max_rows <= 16 && !qk_map && tpw <= 4) {
+    const dim3 g1(nwin, H);
+#define XA1(QZ_, TPW_)                                                                                     \
+  if (pf) k_cross_attn1<T, QZ_, TPW_, true><<<g1, 512, 0, st>>>(q, ldq, ck, cv, Tk, win_row0, win_nrows, win_slot, \
+                                                                win_stride, xq, out, ldo);                       \
+  else k_cross_attn1<T, QZ_, TPW_, false><<<g1, 512, 0, st>>>(q, ldq, ck, cv, Tk, win_row0, win_nrows, win_slot,  \
+                                                              win_stride, xq, out, ldo)
+#define XA1Z(TPW_)                     \
+  switch (xq.part ? xq.z : 0) {        \
+    case 4: XA1(4, TPW_); break;       \
+    case 8: XA1(8, TPW_); break;       \
+    case 10: XA1(10, TPW_); break;     \
+    default: XA1(0, TPW_); break;      \
+  }
+    switch (tpw) {
+      case 1: XA1Z(1) break;
+      case 2: XA1Z(2) break;
+      case 3: XA1Z(3) break;
+      default: XA1Z(4) break;
+    }
+#undef XA1Z
+#undef XA1
+    return;
+  }
   // one 64-key tile per wave, 8 waves per split (3 splits at Tk = 1500: half the
   // partials of 4-wave splits, -75 us per 20-window beam step)
   constexpr int NW = 8;
@@ -723,6 +916,7 @@ void launch_cross_attn(const T* q, int ldq, const T* ck, const T* cv, int Tk, in
   switch (xq.part ? xq.z : 0) {
     case 4: XA(4); break;
     case 8: XA(8); break;
+    case 10: XA(10); break;
     default: XA(0); break;
   }
 #undef XA

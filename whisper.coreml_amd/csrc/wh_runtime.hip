@@ -740,6 +740,7 @@ struct Ctx : public wh_ctx {
       // cross-attention query: in step mode its split-K slabs are reduced inside
       // k_cross_attn (rows per window <= Gcap <= 8), otherwise projected directly
       XQPart xq;
+      if (skinny) xq.max_rows = ancG;
       if (skinny && xq_fused) {
         int ks = 0;
         TRY(partial(xn_d, n, e.wqx, R, n, n, &ks));
