@@ -354,31 +354,39 @@ __global__ __launch_bounds__(256) void k_merge(DecState s, DecOpts o) {
     csrc[tid] = first ? (G - 1) : b;
   }
   __syncthreads();
-  if (tid == 0) {
-    int order[MG_MAXG * KC];
-    for (int c = 0; c < nc; ++c) order[c] = c;
-    // stable sort by score desc (insertion sort keeps insertion order on ties)
-    for (int i = 1; i < nc; ++i) {
-      const int t = order[i];
-      int j = i - 1;
-      while (j >= 0 && csc[order[j]] < csc[t]) { order[j + 1] = order[j]; --j; }
-      order[j + 1] = t;
-    }
-    int saved = 0, nf = 0;
-    for (int q = 0; q < nc && saved < G; ++q) {
-      const int c = order[q];
-      if (ctok[c] == o.eot) {
-        fsc[nf] = csc[c];
-        fsrc[nf] = csrc[c];
-        ++nf;
+  // stable descending sort by rank (ties keep insertion order), then the walk of
+  // decoding.py:375-386 in closed form: the candidate at rank q is taken iff fewer
+  // than G non-EOT candidates rank above it; a non-EOT one becomes beam
+  // #(non-EOT above), an EOT one finished sequence #(EOT above).  One lane per
+  // candidate, no serial loop.
+  __shared__ int rk[MG_MAXG * KC];
+  if (tid < nc) {
+    const float sc = csc[tid];
+    int q = 0;
+    for (int c = 0; c < nc; ++c) q += (csc[c] > sc) || (csc[c] == sc && c < tid);
+    rk[tid] = q;
+  }
+  if (tid == 0) nfin_new = 0;
+  __syncthreads();
+  if (tid < nc) {
+    const int q = rk[tid];
+    int ne = 0, ee = 0;  // non-EOT / EOT candidates ranked above
+    for (int c = 0; c < nc; ++c)
+      if (rk[c] < q) {
+        if (ctok[c] == o.eot) ++ee;
+        else ++ne;
+      }
+    if (ne < G) {
+      if (ctok[tid] == o.eot) {
+        fsc[ee] = csc[tid];
+        fsrc[ee] = csrc[tid];
+        atomicAdd(&nfin_new, 1);
       } else {
-        src[saved] = csrc[c];
-        tok[saved] = ctok[c];
-        s.sum_lp[w * G + saved] = csc[c];
-        ++saved;
+        src[ne] = csrc[tid];
+        tok[ne] = ctok[tid];
+        s.sum_lp[w * G + ne] = csc[tid];
       }
     }
-    nfin_new = nf;
   }
   __syncthreads();
   // new histories / ancestry
