@@ -58,22 +58,28 @@ __global__ __launch_bounds__(256, 2) void k_gemm_tile(GemmArgs a) {
     wsrc[i] = reinterpret_cast<const char*>(W + (int64_t)(n0 + row) * a.K) + col * 16;
     lds_off[i] = row * TROW + col * 16;
   }
-  float4_t xs[4], ws[4];
-  auto gload = [&](int kt) {
+  // two register sets: the global loads of tile kt+2 are in flight while tile kt is
+  // multiplied and tile kt+1 (loaded one step earlier) is written to LDS, so each
+  // load has a whole k-step of MFMAs to land.  Loads are unconditional (the tail
+  // re-reads the last tile) so the compiler's waits stay counted, and the barrier
+  // waits for LDS only — __syncthreads() would drain the tile in flight.
+  float4_t ra[8], rb[8];  // [0..3] X chunks, [4..7] W chunks
+  auto gload = [&](int kt, float4_t* rg) {
     const int kb = kt * TKB;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      xs[i] = *reinterpret_cast<const float4_t*>(xsrc[i] + kb);
-      ws[i] = *reinterpret_cast<const float4_t*>(wsrc[i] + kb);
+      rg[i] = *reinterpret_cast<const float4_t*>(xsrc[i] + kb);
+      rg[4 + i] = *reinterpret_cast<const float4_t*>(wsrc[i] + kb);
     }
   };
-  auto sstore = [&](int buf) {
+  auto sstore = [&](int buf, const float4_t* rg) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      *reinterpret_cast<float4_t*>(&smem[buf][0][lds_off[i]]) = xs[i];
-      *reinterpret_cast<float4_t*>(&smem[buf][1][lds_off[i]]) = ws[i];
+      *reinterpret_cast<float4_t*>(&smem[buf][0][lds_off[i]]) = rg[i];
+      *reinterpret_cast<float4_t*>(&smem[buf][1][lds_off[i]]) = rg[4 + i];
     }
   };
+  auto lds_barrier = [] { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); };
 
   float4_t acc[4][4];
 #pragma unroll
@@ -81,13 +87,7 @@ __global__ __launch_bounds__(256, 2) void k_gemm_tile(GemmArgs a) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = (float4_t){0.f, 0.f, 0.f, 0.f};
 
-  const int nk = a.K / BK;
-  gload(0);
-  sstore(0);
-  __syncthreads();
-  for (int kt = 0; kt < nk; ++kt) {
-    const int buf = kt & 1;
-    if (kt + 1 < nk) gload(kt + 1);
+  auto compute = [&](int buf) {
     const char* As = smem[buf][0];
     const char* Ws = smem[buf][1];
 #pragma unroll
@@ -105,8 +105,25 @@ __global__ __launch_bounds__(256, 2) void k_gemm_tile(GemmArgs a) {
 #pragma unroll
         for (int ni = 0; ni < 4; ++ni) mfma_step(acc[mi][ni], wf[ni], xf[mi]);
     }
-    if (kt + 1 < nk) sstore(buf ^ 1);
-    __syncthreads();
+  };
+
+  const int nk = a.K / BK;
+  gload(0, ra);
+  gload(min(1, nk - 1), rb);
+  sstore(0, ra);
+  lds_barrier();
+  for (int kt = 0; kt < nk; kt += 2) {
+    // LDS buffer 0 holds tile kt, rb holds tile kt+1
+    gload(min(kt + 2, nk - 1), ra);
+    compute(0);
+    if (kt + 1 < nk) sstore(1, rb);
+    lds_barrier();
+    if (kt + 1 >= nk) break;
+    // LDS buffer 1 holds tile kt+1, ra holds tile kt+2
+    gload(min(kt + 3, nk - 1), rb);
+    compute(1);
+    if (kt + 2 < nk) sstore(0, ra);
+    lds_barrier();
   }
 
   // epilogue: lane holds Y[m = m0+wr*64+mi*16+r][n = n0+wc*64+ni*16+4g .. +3]

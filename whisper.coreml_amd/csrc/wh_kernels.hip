@@ -364,7 +364,7 @@ void launch_self_attn(const T* q, int ldq, const T* kc, const T* vc, const int* 
 // at position pos and attends with them directly (no read-back of the fresh row).
 // Only valid when no other row of the launch needs this row's K/V (one row per beam).
 template <typename T>
-__global__ __launch_bounds__(64) void k_self_attn_qkv(const float* __restrict__ part, int nsplit, int64_t part_stride,
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void k_self_attn_qkv(const float* __restrict__ part, int nsplit, int64_t part_stride,
                                                       const float* __restrict__ bqkv, int ns, T* __restrict__ kc,
                                                       T* __restrict__ vc, const int* __restrict__ row_win,
                                                       const int* __restrict__ row_slot, const int* __restrict__ row_pos,
@@ -379,7 +379,13 @@ __global__ __launch_bounds__(64) void k_self_attn_qkv(const float* __restrict__ 
   const int64_t head_stride = (int64_t)ctx * 64;
   const int64_t wbase = (int64_t)w * nbeam;
   auto kv_off = [&](int slot, int p) -> int64_t { return ((wbase + slot) * H + h) * head_stride + (int64_t)p * 64; };
-  // q/k/v of this row and head: lane = d
+  // one round trip for everything that does not depend on this step's projection:
+  // the ancestry slot of every cached key (8 per lane, clamped, issued together) and
+  // the q/k/v partial slabs of this row and head (lane = d)
+  const int plast = max(pos - 1, 0);
+  int sv[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) sv[i] = an[min(lane + 64 * i, plast)];
   float qd, kd, vd;
   {
     const float* pr = part + (int64_t)row * 3 * ns + h * 64 + lane;
@@ -402,32 +408,49 @@ __global__ __launch_bounds__(64) void k_self_attn_qkv(const float* __restrict__ 
         vd += a2[z];
       }
   }
+  for (int i = 0; i < 8; ++i)
+    if (lane + 64 * i < pos) slot_of[lane + 64 * i] = sv[i];
   const T qT = from_f32<T>(qd), kT = from_f32<T>(kd), vT = from_f32<T>(vd);
   kc[kv_off(sl, pos) + lane] = kT;
   vc[kv_off(sl, pos) + lane] = vT;
   qs[lane] = to_f32(qT);
   vs[lane] = to_f32(vT);
   const float s_cur = wave_sum(to_f32(qT) * to_f32(kT));
-  __syncthreads();
+  // the block is one wave: its LDS writes are visible to all its lanes once they have
+  // completed (no barrier, and no wait for the K/V row stores above)
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   float qv[64];
 #pragma unroll
   for (int c = 0; c < 64; ++c) qv[c] = qs[c];
-  // scores of the cached positions p < pos: lane per key
+  // scores of the cached positions p < pos: lane per key, two keys per lane per pass
+  // with all 16 row loads in flight (clamped addresses, no branch around a load)
   float mx = s_cur;
-  for (int p = lane; p < pos; p += 64) {
-    const int slot = an[p];
-    slot_of[p] = slot;
-    const T* kr = kc + kv_off(slot, p);
-    float s = 0.f;
+  for (int p0 = 0; p0 < pos; p0 += 128) {
+    const int pa = min(p0 + lane, plast), pb = min(p0 + 64 + lane, plast);
+    const T* ra = kc + kv_off(slot_of[pa], pa);
+    const T* rb = kc + kv_off(slot_of[pb], pb);
+    Frag<T> ka[8], kb[8];
 #pragma unroll
-    for (int c = 0; c < 64; c += 8) {
-      Frag<T> f;
-      frag_load(f, kr + c);
+    for (int c = 0; c < 8; ++c) frag_load(ka[c], ra + 8 * c);
 #pragma unroll
-      for (int e = 0; e < 8; ++e) s += qv[c + e] * to_f32(f.v[e]);
+    for (int c = 0; c < 8; ++c) frag_load(kb[c], rb + 8 * c);
+    __builtin_amdgcn_sched_barrier(0);  // keep all 16 loads ahead of the math
+    float sa = 0.f, sb = 0.f;
+#pragma unroll
+    for (int c = 0; c < 8; ++c)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        sa += qv[8 * c + e] * to_f32(ka[c].v[e]);
+        sb += qv[8 * c + e] * to_f32(kb[c].v[e]);
+      }
+    if (p0 + lane < pos) {
+      sc[p0 + lane] = sa;
+      mx = fmaxf(mx, sa);
     }
-    sc[p] = s;
-    mx = fmaxf(mx, s);
+    if (p0 + 64 + lane < pos) {
+      sc[p0 + 64 + lane] = sb;
+      mx = fmaxf(mx, sb);
+    }
   }
   mx = wave_max(mx);
   float sum = 0.f;
@@ -438,29 +461,27 @@ __global__ __launch_bounds__(64) void k_self_attn_qkv(const float* __restrict__ 
   }
   const float e_cur = __expf(s_cur - mx);
   sum = wave_sum(sum) + e_cur;
-  __syncthreads();
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  // P.V: lane = (key group kg, 16 B chunk dc); keys kg, kg+8, ... accumulated in order,
+  // 8 per lane in flight (weight 0 past the end)
   const int kg = lane >> 3, dc = (lane & 7) * 8;
   float o[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) o[e] = 0.f;
-  int p = kg;
-  for (; p + 24 < pos; p += 32) {
-    Frag<T> f[4];
+  for (int p0 = kg; p0 < pos; p0 += 64) {
+    Frag<T> f[8];
+    float pw[8];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) frag_load(f[u], vc + kv_off(slot_of[p + 8 * u], p + 8 * u) + dc);
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const float pw = sc[p + 8 * u];
-#pragma unroll
-      for (int e = 0; e < 8; ++e) o[e] += pw * to_f32(f[u].v[e]);
+    for (int u = 0; u < 8; ++u) {
+      const int pc = min(p0 + 8 * u, plast);
+      frag_load(f[u], vc + kv_off(slot_of[pc], pc) + dc);
+      pw[u] = p0 + 8 * u < pos ? sc[pc] : 0.f;
     }
-  }
-  for (; p < pos; p += 8) {
-    Frag<T> f;
-    frag_load(f, vc + kv_off(slot_of[p], p) + dc);
-    const float pw = sc[p];
+    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-    for (int e = 0; e < 8; ++e) o[e] += pw * to_f32(f.v[e]);
+    for (int u = 0; u < 8; ++u)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o[e] += pw[u] * to_f32(f[u].v[e]);
   }
 #pragma unroll
   for (int e = 0; e < 8; ++e) {

@@ -3,11 +3,17 @@
 // Output format is the k_gemv_x EPI_PARTIAL one (fp32 slabs out_f32[z][M][N]), so the
 // consumers (k_resid_ln, k_reduce_store, k_self_attn_qkv) are unchanged.  The tile
 // configuration is picked per shape from a short list: rows in one row group when
-// M <= 112 (MT = ceil(M/16)), then the configuration with the most workgroups that
-// still fits one workgroup per CU (256) — measured on MI355X at 100 rows
-// (tools/proj_bench.hip, profiles/r01/proj_bench.txt): qkv 4.0, out 6.0, fc1 / fc2 11.2
-// -> 8.3 us per launch against k_gemv_x.
+// M <= 112 (MT = ceil(M/16)), then — among tiles of at least 5 k-steps per wave — the
+// configuration with the most workgroups that still fits one workgroup per CU (256).
+// Measured on MI355X at 100 rows (tools/proj_bench.hip, profiles/r01/proj_bench.txt):
+// qkv 4.0, out 6.0, fc1 / fc2 11.2 -> 8.3 us per launch against k_gemv_x; in the
+// large-v3 beam step, 1280 x 1280 at 8 slabs (160 workgroups) instead of 4-step tiles
+// at 10 slabs (200) took the step from 4.20 to 3.97 ms (WHISPER_HIP_PROJ_FORCE sweep,
+// profiles/r01/proj_force_sweep.txt).
+#include <array>
+#include <cstdio>
 #include <cstdlib>
+#include <vector>
 
 #include "wh_proj.h"
 
@@ -16,7 +22,8 @@ namespace wh {
 namespace {
 
 struct Cfg { int nsub, kw, nstep; };
-constexpr Cfg CFGS[] = {{4, 1, 5}, {4, 1, 10}, {5, 1, 10}, {4, 1, 4}, {4, 1, 6}};
+constexpr Cfg CFGS[] = {{4, 1, 5}, {4, 1, 10}, {5, 1, 10}, {4, 1, 4}, {4, 1, 6},
+                        {4, 1, 20}, {5, 1, 20}, {8, 1, 5}, {8, 1, 10}};
 constexpr int NCFG = sizeof(CFGS) / sizeof(CFGS[0]);
 
 typedef void (*KFn)(GemmArgs);
@@ -30,6 +37,7 @@ Ent ent() {
 template <typename T, int MT>
 void row(Ent* e) {
   e[0] = ent<T, MT, 0>(); e[1] = ent<T, MT, 1>(); e[2] = ent<T, MT, 2>(); e[3] = ent<T, MT, 3>(); e[4] = ent<T, MT, 4>();
+  e[5] = ent<T, MT, 5>(); e[6] = ent<T, MT, 6>(); e[7] = ent<T, MT, 7>(); e[8] = ent<T, MT, 8>();
 }
 template <typename T>
 struct Table {
@@ -54,6 +62,23 @@ int launch_proj_partial(const GemmArgs& a, int max_z, hipStream_t st, int* z_out
   }();
   if (off || a.M < 1 || a.M > 112 || a.K % 32 || a.N % 16 || a.x_group_rows < a.M) return -1;
   const int mt = (a.M + 15) / 16, S = a.K / 32;
+  // tuning override: WHISPER_HIP_PROJ_FORCE="N:K:cfg,..." pins the CFGS entry per shape
+  static const std::vector<std::array<int, 3>> force = [] {
+    std::vector<std::array<int, 3>> v;
+    if (const char* e = getenv("WHISPER_HIP_PROJ_FORCE")) {
+      int n, k, c, off = 0, used = 0;
+      while (sscanf(e + off, "%d:%d:%d%n", &n, &k, &c, &used) == 3) {
+        v.push_back({n, k, c});
+        off += used;
+        if (e[off] == ',') ++off;
+        else break;
+      }
+    }
+    return v;
+  }();
+  int forced = -1;
+  for (const auto& f : force)
+    if (f[0] == a.N && f[1] == a.K && f[2] >= 0 && f[2] < NCFG) forced = f[2];
   int best = -1, best_wgs = 0, best_z = 0;
   for (int c = 0; c < NCFG; ++c) {
     const Cfg& k = CFGS[c];
@@ -61,8 +86,19 @@ int launch_proj_partial(const GemmArgs& a, int max_z, hipStream_t st, int* z_out
     const int z = S / (k.kw * k.nstep);
     if (z > max_z || z > 16 || tab.e[mt - 1][c].lds > LDS_MAX) continue;
     const int wgs = (a.N + 16 * k.nsub - 1) / (16 * k.nsub) * z;
+    if (forced >= 0) {
+      if (c == forced) best = c, best_wgs = wgs, best_z = z;
+      continue;
+    }
     if (wgs > 256) continue;
-    if (wgs > best_wgs || (wgs == best_wgs && k.nstep > CFGS[best].nstep)) best = c, best_wgs = wgs, best_z = z;
+    // rank: at least 5 k-steps per wave first (4-step tiles measured 7.8 us against
+    // 5-step tiles' 5.x us in the large-v3 step: 10 slabs instead of 8 and a
+    // latency-bound wave), then the most workgroups, then the longer k-range
+    const bool deep = k.nstep >= 5;
+    const bool bdeep = best >= 0 && CFGS[best].nstep >= 5;
+    if (best < 0 || (deep && !bdeep) ||
+        (deep == bdeep && (wgs > best_wgs || (wgs == best_wgs && k.nstep > CFGS[best].nstep))))
+      best = c, best_wgs = wgs, best_z = z;
   }
   if (best < 0) return -1;
   const Ent& e = tab.e[mt - 1][best];
