@@ -20,15 +20,15 @@ __global__ __launch_bounds__(256) void k_layernorm(const float* __restrict__ x, 
   constexpr int MAXV = 8;  // n <= 64*4*8 = 2048
   float4_t v[MAXV];
   const int nv = n >> 2;
-  float s = 0.f;
 #pragma unroll
   for (int i = 0; i < MAXV; ++i) {
     const int c = lane + 64 * i;
-    if (c < nv) {
-      v[i] = load4f(xr + 4 * c);
-      s += v[i][0] + v[i][1] + v[i][2] + v[i][3];
-    }
+    if (c < nv) v[i] = load4f(xr + 4 * c);
   }
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < MAXV; ++i)
+    if (lane + 64 * i < nv) s += v[i][0] + v[i][1] + v[i][2] + v[i][3];
   const float mean = wave_sum(s) / (float)n;
   float q = 0.f;
 #pragma unroll
@@ -75,11 +75,14 @@ __global__ __launch_bounds__(256) void k_resid_ln(float* __restrict__ x, const f
   float* xr = x + (int64_t)row * n;
   constexpr int MAXV = 2;  // n <= 256 * 4 * 2 = 2048
   const int nv = n >> 2;
-  float4_t v[MAXV];
+  float4_t v[MAXV], gm[MAXV], bt[MAXV];
 #pragma unroll
   for (int i = 0; i < MAXV; ++i) {
     const int c = tid + 256 * i;
     if (c < nv) {
+      // LayerNorm's gamma / beta ride with the first round trip, not after the reductions
+      gm[i] = load4f(gamma + 4 * c);
+      bt[i] = load4f(beta + 4 * c);
       float4_t a = load4f(xr + 4 * c);
       float4_t pp[NS > 0 ? NS : 1];
 #pragma unroll
@@ -121,11 +124,9 @@ __global__ __launch_bounds__(256) void k_resid_ln(float* __restrict__ x, const f
 #pragma unroll
   for (int i = 0; i < MAXV; ++i) {
     const int c = tid + 256 * i;
-    if (c < nv) {
-      const float4_t gm = load4f(gamma + 4 * c), bt = load4f(beta + 4 * c);
-      store4(yr + 4 * c, (v[i][0] - mean) * rstd * gm[0] + bt[0], (v[i][1] - mean) * rstd * gm[1] + bt[1],
-             (v[i][2] - mean) * rstd * gm[2] + bt[2], (v[i][3] - mean) * rstd * gm[3] + bt[3]);
-    }
+    if (c < nv)
+      store4(yr + 4 * c, (v[i][0] - mean) * rstd * gm[i][0] + bt[i][0], (v[i][1] - mean) * rstd * gm[i][1] + bt[i][1],
+             (v[i][2] - mean) * rstd * gm[i][2] + bt[i][2], (v[i][3] - mean) * rstd * gm[i][3] + bt[i][3]);
   }
 }
 
@@ -733,7 +734,7 @@ __global__ __launch_bounds__(64) void k_cross_combine(const float* __restrict__ 
 // tile's K/V fragments in flight while the current tile is computed; the 8 waves'
 // (m, l, O) are merged in LDS and the normalised rows written as T.  <= 16 rows per
 // window (beams of a step), query from q or reduced from split-K slabs (QZ > 0).
-template <typename T, int QZ, int TPW, bool PF>
+template <typename T, int QZ, int TPW, int PF>
 __global__ __launch_bounds__(512, PF ? 1 : 2) void k_cross_attn1(const T* __restrict__ q, int ldq, const T* ck, const T* cvt,
                                                      int Tk, const int* __restrict__ win_row0,
                                                      const int* __restrict__ win_nrows, const int* __restrict__ win_slot,
@@ -766,10 +767,16 @@ __global__ __launch_bounds__(512, PF ? 1 : 2) void k_cross_attn1(const T* __rest
 #pragma unroll
       for (int s = 0; s < 2; ++s) frag_load(vf[dt][s], vbase + (int64_t)(dt * 16 + r) * TKP + kt0 + 32 * s + 8 * g);
   };
-  // PF: the next tile's fragments load while this tile computes (2 register sets,
-  // one workgroup per CU); !PF: one set, two workgroups per CU hide each other
-  Frag<T> kf[PF ? 2 : 1][4][2], vf[PF ? 2 : 1][4][2];
+  // PF 1: the next tile's fragments load while this tile computes (2 register sets,
+  // one workgroup per CU); PF 2: every tile of the wave is loaded up front (one HBM
+  // round trip per workgroup); PF 0: one set, two workgroups per CU hide each other
+  constexpr int NSET = PF == 2 ? TPW : PF == 1 ? 2 : 1;
+  Frag<T> kf[NSET][4][2], vf[NSET][4][2];
   load_kv(0, kf[0], vf[0]);
+  if constexpr (PF == 2) {
+#pragma unroll
+    for (int it = 1; it < TPW; ++it) load_kv(it, kf[it], vf[it]);
+  }
   // the query rows -> LDS
   float4_t qv = (float4_t){0.f, 0.f, 0.f, 0.f};
   {
@@ -801,10 +808,10 @@ __global__ __launch_bounds__(512, PF ? 1 : 2) void k_cross_attn1(const T* __rest
   for (int i = 0; i < 4; ++i) acc[i] = (float4_t){0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int it = 0; it < TPW; ++it) {
-    const int cur = PF ? (it & 1) : 0;
-    if constexpr (PF) {
+    const int cur = PF == 2 ? it : PF == 1 ? (it & 1) : 0;
+    if constexpr (PF == 1) {
       if (it + 1 < TPW) load_kv(it + 1, kf[cur ^ 1], vf[cur ^ 1]);
-    } else {
+    } else if constexpr (PF == 0) {
       if (it > 0) load_kv(it, kf[0], vf[0]);
     }
     const int t = wave + NW * it;
@@ -897,18 +904,20 @@ void launch_cross_attn(const T* q, int ldq, const T* ck, const T* cv, int Tk, in
     const char* e = getenv("WHISPER_HIP_XATTN1");
     return !(e && e[0] == '0');
   }();
-  static const bool pf = [] {
+  static const int pf = [] {
     const char* e = getenv("WHISPER_HIP_XATTN1_PF");
-    return !(e && e[0] == '0');
+    return e ? atoi(e) : 1;
   }();
   const int ntiles = (Tk + 63) / 64, tpw = (ntiles + 7) / 8;
   if (one && xq.max_rows >= 1 && xq.max_rows <= 16 && !qk_map && tpw <= 4) {
     const dim3 g1(nwin, H);
-#define XA1(QZ_, TPW_)                                                                                     \
-  if (pf) k_cross_attn1<T, QZ_, TPW_, true><<<g1, 512, 0, st>>>(q, ldq, ck, cv, Tk, win_row0, win_nrows, win_slot, \
-                                                                win_stride, xq, out, ldo);                       \
-  else k_cross_attn1<T, QZ_, TPW_, false><<<g1, 512, 0, st>>>(q, ldq, ck, cv, Tk, win_row0, win_nrows, win_slot,  \
-                                                              win_stride, xq, out, ldo)
+#define XA1(QZ_, TPW_)                                                                                       \
+  if (pf == 2) k_cross_attn1<T, QZ_, TPW_, 2><<<g1, 512, 0, st>>>(q, ldq, ck, cv, Tk, win_row0, win_nrows, win_slot, \
+                                                                  win_stride, xq, out, ldo);                       \
+  else if (pf == 1) k_cross_attn1<T, QZ_, TPW_, 1><<<g1, 512, 0, st>>>(q, ldq, ck, cv, Tk, win_row0, win_nrows,     \
+                                                                       win_slot, win_stride, xq, out, ldo);         \
+  else k_cross_attn1<T, QZ_, TPW_, 0><<<g1, 512, 0, st>>>(q, ldq, ck, cv, Tk, win_row0, win_nrows, win_slot,        \
+                                                          win_stride, xq, out, ldo)
 #define XA1Z(TPW_)                     \
   switch (xq.part ? xq.z : 0) {        \
     case 4: XA1(4, TPW_); break;       \
