@@ -287,7 +287,7 @@ def main():
                      "achieved": round(gbs(gemv_bytes, gemv_ms), 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(gbs(gemv_bytes, gemv_ms) / HBM_PEAK_GBS, 4),
                      "traffic": traffic, "bytes_per_launch": gemv_bytes, "ms_per_launch": round(gemv_ms, 5)},
-        "roofline_cross_attn": {"bound": "hbm", "kernel": f"k_cross_attn ({n_win} windows x {args.beam} beams)",
+        "roofline_cross_attn": {"bound": "hbm", "kernel": f"k_cross_attn1 ({n_win} windows x {args.beam} beams)",
                                 "achieved": round(gbs(xattn_bytes, xattn_ms), 1), "peak": HBM_PEAK_GBS,
                                 "frac": round(gbs(xattn_bytes, xattn_ms) / HBM_PEAK_GBS, 4),
                                 "bytes_per_launch": xattn_bytes, "ms_per_launch": round(xattn_ms, 5)},

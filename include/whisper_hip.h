@@ -159,7 +159,7 @@ int wh_token_ms(wh_ctx* ctx, float* out, int cap, int* n, int reset);
    the given stage on the context's own stream between HIP events.
    what: 0 = one decoder step graph (current batch), 1 = encoder of 1 window,
          2 = one split-K projection GEMV launch (k_gemv_x; the six per layer, all layers),
-         3 = one cross-attention launch (k_cross_attn, all layers).
+         3 = one cross-attention launch (the step kernel k_cross_attn1, all layers).
    For 2 and 3 *ms_per_iter is the average duration of a single kernel launch. */
 int wh_time_stage(wh_ctx* ctx, int what, int iters, double* ms_per_iter);
 

@@ -31,7 +31,7 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 KERNELS = {
     # short name -> regex on the mangled kernel name
     "k_proj": r"k_projIDF16_",                # fp16 split-K projections (all tile variants)
-    "k_cross_attn": r"k_cross_attnIDF16_",
+    "k_cross_attn1": r"k_cross_attn1IDF16_",      # the step's single-split cross-attention
 }
 
 

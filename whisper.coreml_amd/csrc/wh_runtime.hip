@@ -1259,7 +1259,7 @@ struct Ctx : public wh_ctx {
       // per-launch time of one decoder-step kernel at the current batch, over all
       // layers (so weights / cross-KV stream from HBM as in the step, not from cache):
       // 2 = the six split-K projection GEMVs of each layer (k_gemv_x, EPI_PARTIAL),
-      // 3 = k_cross_attn
+      // 3 = the step's cross-attention (k_cross_attn1)
       if (cur_nwin < 1) return fail(-16, "no decode batch");
       const int R = cur_nwin * cur_G, n = ns;
       int launches = 0;
@@ -1279,8 +1279,10 @@ struct Ctx : public wh_ctx {
           } else {
             const T* ck = ckv + (size_t)(2 * l) * Wcap * TKP * n;
             const T* cv = ckv + (size_t)(2 * l + 1) * Wcap * TKP * n;
+            XQPart xq;  // the step's kernel (k_cross_attn1), query from q_d
+            xq.max_rows = cur_G;
             launch_cross_attn<T>(q_d, n, ck, cv, 1500, nh, NSPLIT, cur_nwin, st_win_row0, st_win_nrows, st_win_slot,
-                                 (int64_t)TKP * n, po, pm, pl, att_d, n, R, nullptr, nullptr, 0, st);
+                                 (int64_t)TKP * n, po, pm, pl, att_d, n, R, nullptr, nullptr, 0, st, xq);
             ++launches;
           }
         }
