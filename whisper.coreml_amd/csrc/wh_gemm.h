@@ -13,6 +13,7 @@ enum Epi {
   EPI_QKV_DEC = 5,     // decoder q -> out[T]; k,v -> self-KV cache at (win, slot, head, pos)
   EPI_F32_COLS = 6,    // logits: out_f32[m][n] (ragged N)
   EPI_PARTIAL = 7,     // split-K partial: out_f32[z][m][n] (no bias; summed by k_resid_ln)
+  EPI_QKV_ENC = 8,     // encoder qkv: q, k -> out[T] (groups); v -> vc as V^T [win][head][64][perm(t)]
 };
 
 struct GemmArgs {
@@ -82,6 +83,21 @@ WH_DEV void epilogue_store(const GemmArgs& a, int m, int gi, int ri, int n, floa
       const int pt = (ri & ~31) + 8 * ((q & 15) >> 2) + 4 * (q >> 4) + (q & 3);
 #pragma unroll
       for (int j = 0; j < 4; ++j) o[(int64_t)(d + j) * a.hs_T + pt] = from_f32<T>(v[j]);
+    }
+  } else if constexpr (EPI == EPI_QKV_ENC) {
+    if (n < 2 * a.hs_state) {
+      T* o = reinterpret_cast<T*>(a.out) + (int64_t)gi * a.out_group_stride + (int64_t)ri * a.ldo + n;
+      store4(o, v[0], v[1], v[2], v[3]);
+    } else {
+      // V transposed per (window, head), keys permuted within 32-key groups as the
+      // cross-KV V^T (EPI_HEADSPLIT): k_attn_enc stages a 64-key tile with 16 B copies
+      // and reads its P.V fragments with one 16 B LDS read each
+      const int c = n - 2 * a.hs_state, h = c >> 6, d = c & 63;
+      const int q = ri & 31;
+      const int pt = (ri & ~31) + 8 * ((q & 15) >> 2) + 4 * (q >> 4) + (q & 3);
+      T* o = reinterpret_cast<T*>(a.vc) + (((int64_t)gi * a.hs_heads + h) * 64 + d) * a.hs_T + pt;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) o[(int64_t)j * a.hs_T] = from_f32<T>(v[j]);
     }
   } else if constexpr (EPI == EPI_QKV_DEC) {
     const int ns = a.hs_state;

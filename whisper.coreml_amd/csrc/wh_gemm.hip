@@ -375,6 +375,7 @@ int launch_gemm(const GemmArgs& a, int epi, hipStream_t st) {
     switch (epi) {
 #define CASE(E) case E: k_gemm_tile<T, E><<<nwg, 256, 0, st>>>(a); break;
       CASE(EPI_STORE) CASE(EPI_STORE_GELU) CASE(EPI_RESID) CASE(EPI_GELU_POS) CASE(EPI_HEADSPLIT) CASE(EPI_QKV_DEC)
+      CASE(EPI_QKV_ENC)
 #undef CASE
       default: return -1;
     }

@@ -13,8 +13,8 @@ template <typename T>
 void launch_resid_ln(float* x, const float* part, int nsplit, int64_t part_stride, const float* bias, T* y,
                      const float* g, const float* b, int rows, int n, float eps, hipStream_t st);
 template <typename T>
-void launch_attn_enc(const T* qkv, int ld, int ns, int H, int Tlen, int nwin, int64_t wsi, T* out, int64_t wso,
-                     hipStream_t st);
+void launch_attn_enc(const T* qkv, int ld, int ns, int H, int Tlen, int nwin, int64_t wsi, const T* vt, int tkp, T* out,
+                     int64_t wso, hipStream_t st);
 template <typename T>
 void launch_self_attn(const T* q, int ldq, const T* kc, const T* vc, const int* rw, const int* rs, const int* rp,
                       const int* anc, int anc_beams, int nbeam, int H, int ctx, T* out, int ldo, int rows,

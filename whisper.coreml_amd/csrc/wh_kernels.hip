@@ -143,20 +143,26 @@ void launch_resid_ln(float* x, const float* part, int nsplit, int64_t part_strid
 }
 
 // ============================================================ encoder flash attention (non-causal)
-// qkv: [T rows][ld] per window (q at col h*64, k at ns + h*64, v at 2ns + h*64); K is
-// pre-scaled by 1/8 (folded into Wk at load, exact).  out: [T][ns] per window.
-// Block = 4 waves x 16 query rows; 64-key tiles staged in LDS (K row-major, V transposed).
+// qkv: [T rows][ld] per window (q at col h*64, k at ns + h*64); K is pre-scaled by 1/8
+// (folded into Wk at load, exact).  vt: V^T per (window, head) [64][tkp] with keys
+// permuted within 32-key groups (EPI_QKV_ENC), so a 64-key tile of V^T is staged with
+// 16 B copies and each P.V fragment is one 16 B LDS read.  The last tile reads 32 keys
+// past tkp (the next row, or 64 elements of slack): finite values under p = 0.
+// out: [T][ns] per window.
+// Block = 4 waves x 16 query rows; 64-key tiles of K (row-major) and V^T in LDS.
 // S^T = K Q^T and O^T = V^T P^T so each lane owns one query row (see wh_common.h).
 template <typename T>
 __global__ __launch_bounds__(256) void k_attn_enc(const T* __restrict__ qkv, int ld, int ns, int Tlen,
-                                                  int64_t win_stride_in, T* __restrict__ out, int64_t win_stride_out) {
+                                                  int64_t win_stride_in, const T* __restrict__ vt, int tkp,
+                                                  T* __restrict__ out, int64_t win_stride_out) {
   constexpr int RS = 64 * (int)sizeof(T) + 16;  // LDS row stride (bytes)
   __shared__ __attribute__((aligned(16))) char Ks[64 * RS];
   __shared__ __attribute__((aligned(16))) char Vt[64 * RS];
-  const int h = blockIdx.y, w = blockIdx.z;
+  const int h = blockIdx.y, w = blockIdx.z, H = gridDim.y;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int r = lane & 15, g = lane >> 4;
   const T* base = qkv + (int64_t)w * win_stride_in;
+  const T* vbase = vt + ((int64_t)w * H + h) * 64 * tkp;
   const int q0 = blockIdx.x * 64 + wave * 16;
   int qrow = q0 + r;
   if (qrow >= Tlen) qrow = Tlen - 1;
@@ -171,20 +177,23 @@ __global__ __launch_bounds__(256) void k_attn_enc(const T* __restrict__ qkv, int
   constexpr float LOG2E = 1.4426950408889634f;
   constexpr int EPC = 16 / (int)sizeof(T);       // elements per 16 B chunk
   constexpr int CPR = 64 / EPC;                   // chunks per 64-element row
+  constexpr int NCH = 64 * CPR / 256;             // chunks per thread per operand
   const int nkb = (Tlen + 63) / 64;
   for (int kb = 0; kb < nkb; ++kb) {
-    // stage: 64 keys x 64 d for K and V
-    for (int c = tid; c < 64 * CPR; c += 256) {
-      const int key = c / CPR, ch = c % CPR;
-      int kr = kb * 64 + key;
-      if (kr >= Tlen) kr = Tlen - 1;
-      const T* src = base + (int64_t)kr * ld + h * 64 + ch * EPC;
-      const float4_t kv = *reinterpret_cast<const float4_t*>(src + ns);
-      *reinterpret_cast<float4_t*>(Ks + key * RS + ch * 16) = kv;
-      const float4_t vv = *reinterpret_cast<const float4_t*>(src + 2 * ns);
-      const T* ve = reinterpret_cast<const T*>(&vv);
+    // stage: 64 keys x 64 d of K, 64 d x 64 (permuted) keys of V^T — all loads first
+    float4_t kv[NCH], vv[NCH];
 #pragma unroll
-      for (int e = 0; e < EPC; ++e) reinterpret_cast<T*>(Vt + (ch * EPC + e) * RS)[key] = ve[e];
+    for (int i = 0; i < NCH; ++i) {
+      const int c = tid + 256 * i, row = c / CPR, ch = c % CPR;
+      const int kr = min(kb * 64 + row, Tlen - 1);
+      kv[i] = *reinterpret_cast<const float4_t*>(base + (int64_t)kr * ld + ns + h * 64 + ch * EPC);
+      vv[i] = *reinterpret_cast<const float4_t*>(vbase + (int64_t)row * tkp + kb * 64 + ch * EPC);
+    }
+#pragma unroll
+    for (int i = 0; i < NCH; ++i) {
+      const int c = tid + 256 * i, row = c / CPR, ch = c % CPR;
+      *reinterpret_cast<float4_t*>(Ks + row * RS + ch * 16) = kv[i];
+      *reinterpret_cast<float4_t*>(Vt + row * RS + ch * 16) = vv[i];
     }
     __syncthreads();
     float4_t sc[4];
@@ -231,13 +240,10 @@ __global__ __launch_bounds__(256) void k_attn_enc(const T* __restrict__ qkv, int
       acc_o[dt] *= alpha;
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
+        // lane (r, g): V^T[d = dt*16 + r][keys 32s + {4g..4g+3, 16+4g..16+4g+3}], which
+        // the permuted layout stores contiguously at 32s + 8g
         Frag<T> vf;
-        const T* vrow = reinterpret_cast<const T*>(Vt + (dt * 16 + r) * RS);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          vf.v[j] = vrow[32 * s + 4 * g + j];
-          vf.v[4 + j] = vrow[32 * s + 16 + 4 * g + j];
-        }
+        frag_load(vf, reinterpret_cast<const T*>(Vt + (dt * 16 + r) * RS) + 32 * s + 8 * g);
         mfma_step(acc_o[dt], vf, pf[s]);
       }
     }
@@ -254,10 +260,10 @@ __global__ __launch_bounds__(256) void k_attn_enc(const T* __restrict__ qkv, int
 }
 
 template <typename T>
-void launch_attn_enc(const T* qkv, int ld, int ns, int H, int Tlen, int nwin, int64_t wsi, T* out, int64_t wso,
-                     hipStream_t st) {
+void launch_attn_enc(const T* qkv, int ld, int ns, int H, int Tlen, int nwin, int64_t wsi, const T* vt, int tkp, T* out,
+                     int64_t wso, hipStream_t st) {
   dim3 grid((Tlen + 63) / 64, H, nwin);
-  k_attn_enc<T><<<grid, 256, 0, st>>>(qkv, ld, ns, Tlen, wsi, out, wso);
+  k_attn_enc<T><<<grid, 256, 0, st>>>(qkv, ld, ns, Tlen, wsi, vt, tkp, out, wso);
 }
 
 // ============================================================ decoder self-attention
@@ -1125,7 +1131,8 @@ void launch_mel_norm(float* mel, int64_t count, int64_t ld, int n_mels, const un
   template void launch_self_attn_qkv<T>(const float*, int, int64_t, const float*, int, T*, T*, const int*, const int*, \
                                         const int*, const int*, int, int, int, int, T*, int, int, hipStream_t);     \
   template void launch_reduce_store<T>(const float*, int, int64_t, const float*, T*, int, int, int, int, hipStream_t); \
-  template void launch_attn_enc<T>(const T*, int, int, int, int, int, int64_t, T*, int64_t, hipStream_t);          \
+  template void launch_attn_enc<T>(const T*, int, int, int, int, int, int64_t, const T*, int, T*, int64_t,         \
+                                   hipStream_t);                                                                    \
   template void launch_self_attn<T>(const T*, int, const T*, const T*, const int*, const int*, const int*,         \
                                     const int*, int, int, int, int, T*, int, int, hipStream_t);                          \
   template void launch_cross_attn<T>(const T*, int, const T*, const T*, int, int, int, int, const int*, const int*, \

@@ -158,7 +158,7 @@ struct Ctx : public wh_ctx {
   std::map<int, float*> d_filters;
 
   // encoder buffers
-  T *melT, *h1, *xn_e, *qkv_e, *att_e, *hm_e, *xa, *ckv;
+  T *melT, *h1, *xn_e, *qkv_e, *vt_e, *att_e, *hm_e, *xa, *ckv;
   float* x_e;
   int64_t* d_seeks;
   int* d_segs;
@@ -274,6 +274,7 @@ struct Ctx : public wh_ctx {
     addA((size_t)WE * MROWS * nm * sizeof(T)); addA((size_t)WE * H1ROWS * n * sizeof(T));
     addA((size_t)WE * 1500 * n * 4); addA((size_t)WE * 1500 * n * sizeof(T)); addA((size_t)WE * 1500 * 3 * n * sizeof(T));
     addA((size_t)WE * 1500 * n * sizeof(T)); addA((size_t)WE * 1500 * 4 * n * sizeof(T));
+    addA(((size_t)WE * nh * 64 * TKP + 64) * sizeof(T));  // encoder V^T (padding keys stay zero)
     addA((size_t)Wcap * 1500 * n * sizeof(T));
     addA((size_t)2 * Ld * Wcap * TKP * n * sizeof(T) + 65536);  // + slack: last key tile reads past TKP
     for (int l = 0; l < Ld; ++l) { addA((size_t)Wcap * Gcap * CTX * n * sizeof(T)); addA((size_t)Wcap * Gcap * CTX * n * sizeof(T)); }
@@ -303,6 +304,7 @@ struct Ctx : public wh_ctx {
     melT = ta((size_t)WE * MROWS * nm); h1 = ta((size_t)WE * H1ROWS * n);
     x_e = fa((size_t)WE * 1500 * n); xn_e = ta((size_t)WE * 1500 * n); qkv_e = ta((size_t)WE * 1500 * 3 * n);
     att_e = ta((size_t)WE * 1500 * n); hm_e = ta((size_t)WE * 1500 * 4 * n);
+    vt_e = ta((size_t)WE * nh * 64 * TKP + 64);  // + the last key tile's read past TKP
     xa = ta((size_t)Wcap * 1500 * n);
     ckv = ta((size_t)2 * Ld * Wcap * TKP * n + 32768 / sizeof(T));
     kc.resize(Ld); vc.resize(Ld);
@@ -581,9 +583,12 @@ struct Ctx : public wh_ctx {
     for (int l = 0; l < La; ++l) {
       auto& e = enc[l];
       launch_layernorm<T>(x_e, xn_e, e.ln1_g, e.ln1_b, M, n, 1e-7f, nullptr, st);
+      // q, k -> qkv_e; v -> vt_e as per-(window, head) V^T with permuted keys
       g = GemmArgs(); g.out = qkv_e; g.ldo = 3 * n;
-      TRY(gemm(xn_e, n, e.wqkv, e.bqkv, M, 3 * n, n, EPI_STORE, g));
-      launch_attn_enc<T>(qkv_e, 3 * n, n, nh, 1500, we, (int64_t)1500 * 3 * n, att_e, (int64_t)1500 * n, st);
+      g.x_group_rows = 1500; g.x_group_stride = (int64_t)1500 * n; g.out_group_stride = (int64_t)1500 * 3 * n;
+      g.hs_state = n; g.hs_heads = nh; g.hs_T = TKP; g.vc = vt_e;
+      TRY(gemm(xn_e, n, e.wqkv, e.bqkv, M, 3 * n, n, EPI_QKV_ENC, g));
+      launch_attn_enc<T>(qkv_e, 3 * n, n, nh, 1500, we, (int64_t)1500 * 3 * n, vt_e, TKP, att_e, (int64_t)1500 * n, st);
       g = GemmArgs(); g.out_f32 = x_e; g.ldo = n;
       TRY(gemm(att_e, n, e.wo, e.bo, M, n, n, EPI_RESID, g));
       launch_layernorm<T>(x_e, xn_e, e.ln2_g, e.ln2_b, M, n, 1e-7f, nullptr, st);
