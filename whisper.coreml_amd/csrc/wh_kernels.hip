@@ -149,121 +149,159 @@ void launch_resid_ln(float* x, const float* part, int nsplit, int64_t part_strid
 // 16 B copies and each P.V fragment is one 16 B LDS read.  The last tile reads 32 keys
 // past tkp (the next row, or 64 elements of slack): finite values under p = 0.
 // out: [T][ns] per window.
-// Block = 4 waves x 16 query rows; 64-key tiles of K (row-major) and V^T in LDS.
-// S^T = K Q^T and O^T = V^T P^T so each lane owns one query row (see wh_common.h).
+// Block = ENC_NW waves x ENC_RT row tiles of 16 queries; each K / V fragment read from
+// LDS feeds ENC_RT MFMAs.  S^T = K Q^T and O^T = V^T P^T so each lane owns one query row per row tile
+// (see wh_common.h).
+constexpr int ENC_RT = 1;  // query row tiles per wave (2 measured 414 us vs 289: 264 VGPRs, one block per CU)
+constexpr int ENC_NW = 8;  // waves per block: the K/V tile staged once for 16 * ENC_NW * ENC_RT queries
 template <typename T>
-__global__ __launch_bounds__(256) void k_attn_enc(const T* __restrict__ qkv, int ld, int ns, int Tlen,
+__global__ __launch_bounds__(64 * ENC_NW) void k_attn_enc(const T* __restrict__ qkv, int ld, int ns, int Tlen,
                                                   int64_t win_stride_in, const T* __restrict__ vt, int tkp,
                                                   T* __restrict__ out, int64_t win_stride_out) {
+  constexpr int RT = ENC_RT, NT = 64 * ENC_NW;
   constexpr int RS = 64 * (int)sizeof(T) + 16;  // LDS row stride (bytes)
-  __shared__ __attribute__((aligned(16))) char Ks[64 * RS];
-  __shared__ __attribute__((aligned(16))) char Vt[64 * RS];
+  __shared__ __attribute__((aligned(16))) char Ks[2][64 * RS];
+  __shared__ __attribute__((aligned(16))) char Vt[2][64 * RS];
   const int h = blockIdx.y, w = blockIdx.z, H = gridDim.y;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int r = lane & 15, g = lane >> 4;
   const T* base = qkv + (int64_t)w * win_stride_in;
   const T* vbase = vt + ((int64_t)w * H + h) * 64 * tkp;
-  const int q0 = blockIdx.x * 64 + wave * 16;
-  int qrow = q0 + r;
-  if (qrow >= Tlen) qrow = Tlen - 1;
-  Frag<T> qf[2];
-  frag_load(qf[0], base + (int64_t)qrow * ld + h * 64 + 8 * g);
-  frag_load(qf[1], base + (int64_t)qrow * ld + h * 64 + 32 + 8 * g);
-
-  float4_t acc_o[4];
+  const int q0 = blockIdx.x * 16 * ENC_NW * RT + wave * 16 * RT;
+  Frag<T> qf[RT][2];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) acc_o[i] = (float4_t){0.f, 0.f, 0.f, 0.f};
-  float m_run = -INFINITY, l_run = 0.f;
+  for (int t = 0; t < RT; ++t) {
+    const int qrow = min(q0 + 16 * t + r, Tlen - 1);
+    frag_load(qf[t][0], base + (int64_t)qrow * ld + h * 64 + 8 * g);
+    frag_load(qf[t][1], base + (int64_t)qrow * ld + h * 64 + 32 + 8 * g);
+  }
+
+  float4_t acc_o[RT][4];
+  float m_run[RT], l_run[RT];
+#pragma unroll
+  for (int t = 0; t < RT; ++t) {
+    m_run[t] = -INFINITY;
+    l_run[t] = 0.f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) acc_o[t][i] = (float4_t){0.f, 0.f, 0.f, 0.f};
+  }
   constexpr float LOG2E = 1.4426950408889634f;
   constexpr int EPC = 16 / (int)sizeof(T);       // elements per 16 B chunk
   constexpr int CPR = 64 / EPC;                   // chunks per 64-element row
-  constexpr int NCH = 64 * CPR / 256;             // chunks per thread per operand
+  constexpr int NCH = 64 * CPR / NT;              // chunks per thread per operand
   const int nkb = (Tlen + 63) / 64;
-  for (int kb = 0; kb < nkb; ++kb) {
-    // stage: 64 keys x 64 d of K, 64 d x 64 (permuted) keys of V^T — all loads first
-    float4_t kv[NCH], vv[NCH];
+  // 64 keys x 64 d of K and 64 d x 64 (permuted) keys of V^T per tile; the next tile's
+  // loads are in flight while this one is computed (double-buffered LDS, one barrier
+  // per tile that waits for LDS only, so the prefetch stays in flight)
+  float4_t kv[NCH], vv[NCH];
+  auto load_tile = [&](int kb) {
 #pragma unroll
     for (int i = 0; i < NCH; ++i) {
-      const int c = tid + 256 * i, row = c / CPR, ch = c % CPR;
+      const int c = tid + NT * i, row = c / CPR, ch = c % CPR;
       const int kr = min(kb * 64 + row, Tlen - 1);
       kv[i] = *reinterpret_cast<const float4_t*>(base + (int64_t)kr * ld + ns + h * 64 + ch * EPC);
       vv[i] = *reinterpret_cast<const float4_t*>(vbase + (int64_t)row * tkp + kb * 64 + ch * EPC);
     }
+  };
+  auto store_tile = [&](int buf) {
 #pragma unroll
     for (int i = 0; i < NCH; ++i) {
-      const int c = tid + 256 * i, row = c / CPR, ch = c % CPR;
-      *reinterpret_cast<float4_t*>(Ks + row * RS + ch * 16) = kv[i];
-      *reinterpret_cast<float4_t*>(Vt + row * RS + ch * 16) = vv[i];
+      const int c = tid + NT * i, row = c / CPR, ch = c % CPR;
+      *reinterpret_cast<float4_t*>(Ks[buf] + row * RS + ch * 16) = kv[i];
+      *reinterpret_cast<float4_t*>(Vt[buf] + row * RS + ch * 16) = vv[i];
     }
-    __syncthreads();
-    float4_t sc[4];
+  };
+  load_tile(0);
+  store_tile(0);
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  for (int kb = 0; kb < nkb; ++kb) {
+    const int buf = kb & 1;
+    load_tile(min(kb + 1, nkb - 1));
+    const char* Kb = Ks[buf];
+    const char* Vb = Vt[buf];
+    float4_t sc[RT][4];
 #pragma unroll
-    for (int kt = 0; kt < 4; ++kt) {
-      sc[kt] = (float4_t){0.f, 0.f, 0.f, 0.f};
+    for (int t = 0; t < RT; ++t)
+#pragma unroll
+      for (int kt = 0; kt < 4; ++kt) sc[t][kt] = (float4_t){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kt = 0; kt < 4; ++kt)
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
         Frag<T> kf;
-        frag_load(kf, reinterpret_cast<const T*>(Ks + (kt * 16 + r) * RS) + 32 * s + 8 * g);
-        mfma_step(sc[kt], kf, qf[s]);
+        frag_load(kf, reinterpret_cast<const T*>(Kb + (kt * 16 + r) * RS) + 32 * s + 8 * g);
+#pragma unroll
+        for (int t = 0; t < RT; ++t) mfma_step(sc[t][kt], kf, qf[t][s]);
       }
+    Frag<T> pf[RT][2];
+    float alpha[RT];
+#pragma unroll
+    for (int t = 0; t < RT; ++t) {
+      // mask ragged last tile; row max over the 64 keys
+      float mx = -INFINITY;
+#pragma unroll
+      for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int key = kb * 64 + kt * 16 + 4 * g + j;
+          if (key >= Tlen) sc[t][kt][j] = -INFINITY;
+          mx = fmaxf(mx, sc[t][kt][j]);
+        }
+      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      const float m_new = fmaxf(m_run[t], mx);
+      alpha[t] = exp2f((m_run[t] - m_new) * LOG2E);
+      float ps = 0.f;
+#pragma unroll
+      for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const float p = exp2f((sc[t][kt][j] - m_new) * LOG2E);
+          ps += p;
+          pf[t][kt >> 1].v[(kt & 1) * 4 + j] = from_f32<T>(p);
+        }
+      ps += __shfl_xor(ps, 16, 64);
+      ps += __shfl_xor(ps, 32, 64);
+      l_run[t] = l_run[t] * alpha[t] + ps;
+      m_run[t] = m_new;
     }
-    // mask ragged last tile; block row max over the 64 keys
-    float mx = -INFINITY;
-#pragma unroll
-    for (int kt = 0; kt < 4; ++kt)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int key = kb * 64 + kt * 16 + 4 * g + j;
-        if (key >= Tlen) sc[kt][j] = -INFINITY;
-        mx = fmaxf(mx, sc[kt][j]);
-      }
-    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-    const float m_new = fmaxf(m_run, mx);
-    const float alpha = exp2f((m_run - m_new) * LOG2E);
-    float ps = 0.f;
-    Frag<T> pf[2];
-#pragma unroll
-    for (int kt = 0; kt < 4; ++kt)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const float p = exp2f((sc[kt][j] - m_new) * LOG2E);
-        ps += p;
-        pf[kt >> 1].v[(kt & 1) * 4 + j] = from_f32<T>(p);
-      }
-    ps += __shfl_xor(ps, 16, 64);
-    ps += __shfl_xor(ps, 32, 64);
-    l_run = l_run * alpha + ps;
-    m_run = m_new;
 #pragma unroll
     for (int dt = 0; dt < 4; ++dt) {
-      acc_o[dt] *= alpha;
+#pragma unroll
+      for (int t = 0; t < RT; ++t) acc_o[t][dt] *= alpha[t];
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
         // lane (r, g): V^T[d = dt*16 + r][keys 32s + {4g..4g+3, 16+4g..16+4g+3}], which
         // the permuted layout stores contiguously at 32s + 8g
         Frag<T> vf;
-        frag_load(vf, reinterpret_cast<const T*>(Vt + (dt * 16 + r) * RS) + 32 * s + 8 * g);
-        mfma_step(acc_o[dt], vf, pf[s]);
+        frag_load(vf, reinterpret_cast<const T*>(Vb + (dt * 16 + r) * RS) + 32 * s + 8 * g);
+#pragma unroll
+        for (int t = 0; t < RT; ++t) mfma_step(acc_o[t][dt], vf, pf[t][s]);
       }
     }
-    __syncthreads();
+    store_tile(buf ^ 1);  // buffer last read in the previous tile, before that barrier
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
   }
-  const int q = q0 + r;
-  if (q < Tlen) {
-    const float inv = 1.f / l_run;
-    T* o = out + (int64_t)w * win_stride_out + (int64_t)q * ns + h * 64;
 #pragma unroll
-    for (int dt = 0; dt < 4; ++dt)
-      store4(o + dt * 16 + 4 * g, acc_o[dt][0] * inv, acc_o[dt][1] * inv, acc_o[dt][2] * inv, acc_o[dt][3] * inv);
+  for (int t = 0; t < RT; ++t) {
+    const int q = q0 + 16 * t + r;
+    if (q < Tlen) {
+      const float inv = 1.f / l_run[t];
+      T* o = out + (int64_t)w * win_stride_out + (int64_t)q * ns + h * 64;
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt)
+        store4(o + dt * 16 + 4 * g, acc_o[t][dt][0] * inv, acc_o[t][dt][1] * inv, acc_o[t][dt][2] * inv,
+               acc_o[t][dt][3] * inv);
+    }
   }
 }
 
 template <typename T>
 void launch_attn_enc(const T* qkv, int ld, int ns, int H, int Tlen, int nwin, int64_t wsi, const T* vt, int tkp, T* out,
                      int64_t wso, hipStream_t st) {
-  dim3 grid((Tlen + 63) / 64, H, nwin);
-  k_attn_enc<T><<<grid, 256, 0, st>>>(qkv, ld, ns, Tlen, wsi, vt, tkp, out, wso);
+  constexpr int QB = 16 * ENC_NW * ENC_RT;
+  dim3 grid((Tlen + QB - 1) / QB, H, nwin);
+  k_attn_enc<T><<<grid, 64 * ENC_NW, 0, st>>>(qkv, ld, ns, Tlen, wsi, vt, tkp, out, wso);
 }
 
 // ============================================================ decoder self-attention
