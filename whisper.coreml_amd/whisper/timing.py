@@ -72,7 +72,7 @@ def find_alignment_batch(model: "Whisper", tokenizer: Tokenizer, text_tokens: Li
 def _words_from_path(tokenizer: Tokenizer, text_tokens: List[int], probs: np.ndarray, text_indices: np.ndarray,
                      time_indices: np.ndarray) -> List[WordTiming]:
     """timing.py:208-231 on the device results."""
-    text_token_probs = probs.astype(np.float64).tolist()
+    text_token_probs = probs.astype(np.float64)
     words, word_tokens = tokenizer.split_to_word_tokens(text_tokens + [tokenizer.eot])
     if len(word_tokens) <= 1:
         return []
@@ -80,9 +80,14 @@ def _words_from_path(tokenizer: Tokenizer, text_tokens: List[int], probs: np.nda
 
     jumps = np.pad(np.diff(text_indices), (1, 0), constant_values=1).astype(bool)
     jump_times = time_indices[jumps] / TOKENS_PER_SECOND
-    start_times = jump_times[word_boundaries[:-1]]
-    end_times = jump_times[word_boundaries[1:]]
-    word_probabilities = [np.mean(text_token_probs[i:j]) for i, j in zip(word_boundaries[:-1], word_boundaries[1:])]
+    start_times = jump_times[word_boundaries[:-1]].tolist()
+    end_times = jump_times[word_boundaries[1:]].tolist()
+    # per-word mean probability (np.mean over each word's tokens, timing.py:221-224),
+    # as segment sums in one pass: equal to the per-word np.mean up to summation order
+    lo, hi = word_boundaries[:-1], word_boundaries[1:]
+    csum = np.concatenate(([0.0], np.cumsum(text_token_probs)))
+    n = hi - lo
+    word_probabilities = np.where(n > 0, (csum[hi] - csum[lo]) / np.maximum(n, 1), np.nan).tolist()
 
     return [WordTiming(word, tokens, start, end, probability)
             for word, tokens, start, end, probability in zip(words, word_tokens, start_times, end_times,
