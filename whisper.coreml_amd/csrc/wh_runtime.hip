@@ -47,7 +47,15 @@ namespace {
 constexpr int CTX = 448;          // text positions (decoder.py:243, decoding.py:173)
 constexpr int HCTX = CTX + 1;     // history capacity (tokens.shape[-1] may reach n_ctx + 1)
 constexpr int NSPLIT = 8;         // cross-attention key splits (1500 / 8 = 188 keys)
-constexpr int ENC_CHUNK = 16;     // encoder windows per pass
+// encoder windows per pass (WHISPER_HIP_ENC_CHUNK overrides; activations scale with it)
+static int enc_chunk() {
+  static const int v = [] {
+    const char* e = getenv("WHISPER_HIP_ENC_CHUNK");
+    const int c = e ? atoi(e) : 16;
+    return c >= 1 && c <= 64 ? c : 16;
+  }();
+  return v;
+}
 constexpr int PRE_ROWS = 1024;    // min prefill rows per pass (the context sizes it to ~240 per window)
 constexpr int MROWS = 3008;       // melT rows per window (1 pad + 3000 + slack for padded conv1 K)
 constexpr int H1ROWS = 3002;      // conv1 output rows per window (zero rows 0 and 3001)
@@ -263,7 +271,7 @@ struct Ctx : public wh_ctx {
     if (!ckv_b) return fail(-3, "weight arena overflow");
     expected = 5 + La * 15 + 2 + 2 + Ld * 24 + 2;
     // ---------------- activations
-    const int WE = std::min(Wcap, ENC_CHUNK);
+    const int WE = std::min(Wcap, enc_chunk());
     // first-pass rows per pass: every window's word-timestamp alignment (<= ~230 tokens)
     // fits one pass, so its GEMMs run at M in the thousands
     PRE = std::max(PRE_ROWS, std::min(Wcap * 240, 8192));
@@ -621,7 +629,7 @@ struct Ctx : public wh_ctx {
     hipEventRecord(tm.a, st);
     HIPCHK(hipMemcpyAsync(d_seeks, h_seeks.data(), n_win * 8, hipMemcpyHostToDevice, st));
     HIPCHK(hipMemcpyAsync(d_segs, segs, n_win * 4, hipMemcpyHostToDevice, st));
-    const int WE = std::min(Wcap, ENC_CHUNK);
+    const int WE = std::min(Wcap, enc_chunk());
     for (int s0 = 0; s0 < n_win; s0 += WE) TRY(encode_chunk(s0, std::min(WE, n_win - s0)));
     hipEventRecord(tm.b, st);
     HIPCHK(hipStreamSynchronize(st));
