@@ -189,6 +189,7 @@ struct Ctx : public wh_ctx {
   hipGraphExec_t gexec = nullptr;
   std::vector<char> graph_key;
   int* h_done = nullptr;
+  hipEvent_t poll_ev[2] = {nullptr, nullptr};
 
   Timer tm;
 
@@ -203,6 +204,8 @@ struct Ctx : public wh_ctx {
     for (auto& kv : d_filters) hipFree(kv.second);
     if (d_gmax) hipFree(d_gmax);
     if (h_done) hipHostFree(h_done);
+    for (auto& e : poll_ev)
+      if (e) hipEventDestroy(e);
   }
 
   int init(int device_, const wh_dims& dims, int Wcap_, int Gcap_) {
@@ -227,7 +230,8 @@ struct Ctx : public wh_ctx {
     HIPCHK(hipSetDevice(device));
     HIPCHK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
     tm.create();
-    HIPCHK(hipHostMalloc((void**)&h_done, sizeof(int) * Wcap));
+    HIPCHK(hipHostMalloc((void**)&h_done, sizeof(int) * 2 * Wcap));  // two poll buffers
+    for (auto& e : poll_ev) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     // ---------------- weights
     const size_t n = ns;
     size_t wb = 0;
@@ -986,20 +990,35 @@ struct Ctx : public wh_ctx {
     hipEventRecord(tm.a, st);
     int steps = 0, done = 0;
     const int chunk = 8;
-    auto tc = std::chrono::steady_clock::now();
-    while (steps < max_steps) {
+    // chunks of `chunk` steps, each followed by an async copy of the done flags; the
+    // next chunk is queued before the host waits for the previous chunk's flags, so
+    // the GPU never idles on the poll (at most one chunk of no-op steps after the last
+    // window finishes: finished windows' rows are clamped and skipped by the selection)
+    auto queue_chunk = [&](int b) -> int {
       const int k = std::min(chunk, max_steps - steps);
       for (int i = 0; i < k; ++i) TRY(launch_step());
       steps += k;
-      HIPCHK(hipMemcpyAsync(h_done, S.done, cur_nwin * 4, hipMemcpyDeviceToHost, st));
-      HIPCHK(hipStreamSynchronize(st));
-      // per-token wall time of this chunk (graph launches + done poll), for the p50
+      HIPCHK(hipMemcpyAsync(h_done + b * Wcap, S.done, cur_nwin * 4, hipMemcpyDeviceToHost, st));
+      HIPCHK(hipEventRecord(poll_ev[b], st));
+      return k;
+    };
+    auto tc = std::chrono::steady_clock::now();
+    int b = 0, kq[2] = {0, 0};
+    kq[0] = queue_chunk(0);
+    if (kq[0] < 0) return kq[0];
+    while (true) {
+      const int nb = b ^ 1;
+      kq[nb] = steps < max_steps ? queue_chunk(nb) : 0;
+      if (kq[nb] < 0) return kq[nb];
+      HIPCHK(hipEventSynchronize(poll_ev[b]));
+      // per-token wall time (graph launches + done poll, pipelined), for the p50
       const auto now = std::chrono::steady_clock::now();
-      token_ms.push_back((float)(std::chrono::duration<double, std::milli>(now - tc).count() / k));
+      token_ms.push_back((float)(std::chrono::duration<double, std::milli>(now - tc).count() / kq[b]));
       tc = now;
       done = 0;
-      for (int w = 0; w < cur_nwin; ++w) done += h_done[w] != 0;
-      if (done == cur_nwin) break;
+      for (int w = 0; w < cur_nwin; ++w) done += h_done[b * Wcap + w] != 0;
+      if (done == cur_nwin || kq[nb] == 0) break;
+      b = nb;
     }
     hipEventRecord(tm.b, st);
     HIPCHK(hipStreamSynchronize(st));
