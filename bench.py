@@ -247,7 +247,11 @@ def main():
     task = DecodingTask(model, whisper.DecodingOptions(language="en", beam_size=args.beam))
     model.ctx.decode_begin(task.wh_opts(), [task.initial_tokens] * n_win, [task.sot_index] * n_win)
     rows = n_win * args.beam
-    gemv_ms = model.ctx.time_stage(2, 3)
+    # in-step: every k_proj of 3 eager steps bracketed by HIP events on the context
+    # stream, each behind its real producer kernel (what rocprof sees in the step);
+    # back-to-back: the same launches queued without their producers (time_stage 2)
+    gemv_ms = model.ctx.time_stage(7, 3)
+    gemv_b2b_ms = model.ctx.time_stage(2, 3)
     gemv_bytes = projection_bytes_per_launch(dims, rows)
     xattn_ms = model.ctx.time_stage(3, 3)
     xattn_bytes = cross_attn_bytes_per_launch(dims, n_win, rows)
@@ -286,7 +290,9 @@ def main():
                                                 f"per decoder layer)",
                      "achieved": round(gbs(gemv_bytes, gemv_ms), 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(gbs(gemv_bytes, gemv_ms) / HBM_PEAK_GBS, 4),
-                     "traffic": traffic, "bytes_per_launch": gemv_bytes, "ms_per_launch": round(gemv_ms, 5)},
+                     "traffic": traffic, "bytes_per_launch": gemv_bytes, "ms_per_launch": round(gemv_ms, 5),
+                     "timing": "HIP events around each launch inside eager decoder steps",
+                     "ms_per_launch_back_to_back": round(gemv_b2b_ms, 5)},
         "roofline_cross_attn": {"bound": "hbm", "kernel": f"k_cross_attn1 ({n_win} windows x {args.beam} beams)",
                                 "achieved": round(gbs(xattn_bytes, xattn_ms), 1), "peak": HBM_PEAK_GBS,
                                 "frac": round(gbs(xattn_bytes, xattn_ms) / HBM_PEAK_GBS, 4),

@@ -40,6 +40,28 @@ WH_DEV void frag_load(Frag<float>& f, const float* p) {
   f.v = (float8_t){a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
 }
 
+// once-read streams (decode weights, cross-K/V): nontemporal loads when built with
+// WH_NT=1 (MI355X_MICROARCH.md "nt-weights")
+#ifndef WH_NT
+#define WH_NT 0
+#endif
+WH_DEV void frag_load_stream(Frag<half_t>& f, const half_t* p) {
+#if WH_NT
+  f.v = __builtin_nontemporal_load(reinterpret_cast<const half8_t*>(p));
+#else
+  frag_load(f, p);
+#endif
+}
+WH_DEV void frag_load_stream(Frag<float>& f, const float* p) {
+#if WH_NT
+  const float4_t* q = reinterpret_cast<const float4_t*>(p);
+  float4_t a = __builtin_nontemporal_load(q), b = __builtin_nontemporal_load(q + 1);
+  f.v = (float8_t){a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+#else
+  frag_load(f, p);
+#endif
+}
+
 // two groups of 4 consecutive elements (8 B each for half, 16 B for float)
 WH_DEV void load4x2(Frag<half_t>& f, const half_t* p0, const half_t* p1) {
   const half4_t a = *reinterpret_cast<const half4_t*>(p0), b = *reinterpret_cast<const half4_t*>(p1);

@@ -121,7 +121,10 @@ int launch_gemm(const GemmArgs& a, int epi, hipStream_t st);
 // out_f32[z][M][N]; returns 0 and the split count, or < 0 when no tile configuration
 // fits the shape (callers then use launch_gemm's EPI_PARTIAL path)
 template <typename T>
-int launch_proj_partial(const GemmArgs& a, int max_z, hipStream_t st, int* z_out);
+// ev0/ev1 (optional): timestamps of the kernel's own dispatch (hipExtLaunchKernelGGL),
+// i.e. its execution time as a profiler sees it, with no marker packets around it
+int launch_proj_partial(const GemmArgs& a, int max_z, hipStream_t st, int* z_out, hipEvent_t ev0 = nullptr,
+                        hipEvent_t ev1 = nullptr);
 
 // split-K factor the skinny paths use for EPI_PARTIAL at this shape (<= min(16, max_z))
 int gemv_ksplit(int M, int N, int K, int max_z = 16, int mt_block = 0);

@@ -282,7 +282,7 @@ __global__ __launch_bounds__(64 * NW) void k_gemv_x(GemmArgs a) {
     const int ns = min(KCH, Kc - kc) / 32;
     const int cpr = ns * 2 * (int)sizeof(T);  // valid 16 B chunks per row
 #pragma unroll
-    for (int s = 0; s < KS; ++s) frag_load(w[s], wp + kc + min(s, ns - 1) * 32);
+    for (int s = 0; s < KS; ++s) frag_load_stream(w[s], wp + kc + min(s, ns - 1) * 32);
 #pragma unroll
     for (int i = 0; i < NCH; ++i) {
       const int ch = (tid + NT * i) % CPR;

@@ -803,13 +803,13 @@ __global__ __launch_bounds__(512, PF ? 1 : 2) void k_cross_attn1(const T* __rest
 #pragma unroll
     for (int kt = 0; kt < 4; ++kt) {
       const T* kp = kbase + (int64_t)(kt0 + kt * 16 + r) * 64 + 8 * g;
-      frag_load(kf[kt][0], kp);
-      frag_load(kf[kt][1], kp + 32);
+      frag_load_stream(kf[kt][0], kp);
+      frag_load_stream(kf[kt][1], kp + 32);
     }
 #pragma unroll
     for (int dt = 0; dt < 4; ++dt)
 #pragma unroll
-      for (int s = 0; s < 2; ++s) frag_load(vf[dt][s], vbase + (int64_t)(dt * 16 + r) * TKP + kt0 + 32 * s + 8 * g);
+      for (int s = 0; s < 2; ++s) frag_load_stream(vf[dt][s], vbase + (int64_t)(dt * 16 + r) * TKP + kt0 + 32 * s + 8 * g);
   };
   // PF 1: the next tile's fragments load while this tile computes (2 register sets,
   // one workgroup per CU); PF 2: every tile of the wave is loaded up front (one HBM

@@ -73,7 +73,7 @@ __global__ __launch_bounds__(64 * NSUB * KW) void k_proj(GemmArgs a) {
   const T* wp = reinterpret_cast<const T*>(a.W) + (int64_t)min(n0 + r, a.N - 1) * a.K + kb + kw * NSTEP * 32 + 8 * g;
   Frag<T> wf[NSTEP];
 #pragma unroll
-  for (int s = 0; s < NSTEP; ++s) frag_load(wf[s], wp + s * 32);
+  for (int s = 0; s < NSTEP; ++s) frag_load_stream(wf[s], wp + s * 32);
   // 3. X -> LDS
 #pragma unroll
   for (int i = 0; i < P::XC; ++i) {

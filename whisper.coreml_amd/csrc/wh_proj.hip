@@ -16,6 +16,7 @@
 #include <vector>
 
 #include "wh_proj.h"
+#include <hip/hip_ext.h>
 
 namespace wh {
 
@@ -54,7 +55,7 @@ constexpr int LDS_MAX = 160 * 1024;
 }  // namespace
 
 template <typename T>
-int launch_proj_partial(const GemmArgs& a, int max_z, hipStream_t st, int* z_out) {
+int launch_proj_partial(const GemmArgs& a, int max_z, hipStream_t st, int* z_out, hipEvent_t ev0, hipEvent_t ev1) {
   static Table<T> tab;
   static const bool off = [] {
     const char* e = getenv("WHISPER_HIP_PROJ");
@@ -110,12 +111,15 @@ int launch_proj_partial(const GemmArgs& a, int max_z, hipStream_t st, int* z_out
   }
   GemmArgs b = a;
   b.ksplit = best_z;
-  hipLaunchKernelGGL(e.f, dim3(best_wgs), dim3(64 * CFGS[best].nsub * CFGS[best].kw), e.lds, st, b);
+  if (ev0)
+    hipExtLaunchKernelGGL(e.f, dim3(best_wgs), dim3(64 * CFGS[best].nsub * CFGS[best].kw), e.lds, st, ev0, ev1, 0, b);
+  else
+    hipLaunchKernelGGL(e.f, dim3(best_wgs), dim3(64 * CFGS[best].nsub * CFGS[best].kw), e.lds, st, b);
   *z_out = best_z;
   return 0;
 }
 
-template int launch_proj_partial<float>(const GemmArgs&, int, hipStream_t, int*);
-template int launch_proj_partial<half_t>(const GemmArgs&, int, hipStream_t, int*);
+template int launch_proj_partial<float>(const GemmArgs&, int, hipStream_t, int*, hipEvent_t, hipEvent_t);
+template int launch_proj_partial<half_t>(const GemmArgs&, int, hipStream_t, int*, hipEvent_t, hipEvent_t);
 
 }  // namespace wh

@@ -192,6 +192,8 @@ struct Ctx : public wh_ctx {
   hipEvent_t poll_ev[2] = {nullptr, nullptr};
 
   Timer tm;
+  std::vector<hipEvent_t> proj_ev;  // time_stage(7) event pairs, empty otherwise
+  int proj_ev_n = 0;
 
   ~Ctx() override {
     if (gexec) hipGraphExecDestroy(gexec);
@@ -690,7 +692,11 @@ struct Ctx : public wh_ctx {
     g.X = X; g.ldx = ldx; g.W = W; g.M = R; g.N = N; g.K = K; g.x_group_rows = R;
     g.out_f32 = part; g.ldo = N;
     const int maxz = part_slabs(R, N);
-    const int rc = launch_proj_partial<T>(g, maxz, st, ks);
+    // time_stage(7): each k_proj of an eager step timed by its own dispatch events
+    const bool tev = proj_ev_n < (int)proj_ev.size() / 2;
+    const int rc = tev ? launch_proj_partial<T>(g, maxz, st, ks, proj_ev[2 * proj_ev_n], proj_ev[2 * proj_ev_n + 1])
+                       : launch_proj_partial<T>(g, maxz, st, ks);
+    if (tev && rc == 0) ++proj_ev_n;
     if (rc == 0) return 0;
     if (rc != -1) return fail(-20, "k_proj launch failed code " + std::to_string(rc));
     *ks = gemv_ksplit(R, N, K, maxz);
@@ -1287,17 +1293,21 @@ struct Ctx : public wh_ctx {
       hipEventRecord(tm.a, st);
       for (int i = 0; i < iters; ++i) TRY(encode_chunk(0, 1));
       hipEventRecord(tm.b, st);
-    } else if (what == 2 || what == 3) {
+    } else if (what == 2 || what == 3 || what == 5 || what == 6) {
       // per-launch time of one decoder-step kernel at the current batch, over all
       // layers (so weights / cross-KV stream from HBM as in the step, not from cache):
       // 2 = the six split-K projection GEMVs of each layer (k_gemv_x, EPI_PARTIAL),
       // 3 = the step's cross-attention (k_cross_attn1)
+      // 5 / 6 = 2 / 3 on layer 0 only, repeated (operands Infinity-Cache warm)
       if (cur_nwin < 1) return fail(-16, "no decode batch");
+      const bool warm = what >= 5;
+      if (warm) what -= 3;
+      const int nl = warm ? 1 : Ld;
       const int R = cur_nwin * cur_G, n = ns;
       int launches = 0;
       hipEventRecord(tm.a, st);
-      for (int i = 0; i < iters; ++i)
-        for (int l = 0; l < Ld; ++l) {
+      for (int i = 0; i < iters * (warm ? Ld : 1); ++i)
+        for (int l = 0; l < nl; ++l) {
           auto& e = dec[l];
           if (what == 2) {
             struct P { const T* X; int K; const T* W; int N; } ps[6] = {
@@ -1323,6 +1333,33 @@ struct Ctx : public wh_ctx {
       float t = 0;
       hipEventElapsedTime(&t, tm.a, tm.b);
       *ms = t / launches;
+      return 0;
+    } else if (what == 7) {
+      // per-launch time of the step's k_proj projections inside eager steps: every
+      // launch carries its own start/stop events (hipExtLaunchKernelGGL: timestamps of
+      // the dispatch itself, no marker packets), in the step's kernel order, so each
+      // one runs behind its real producer as in the graph (not back to back)
+      if (cur_nwin < 1) return fail(-16, "no decode batch");
+      const int per_step = 6 * Ld;
+      proj_ev.resize(2 * per_step * iters);
+      for (auto& ev : proj_ev) HIPCHK(hipEventCreate(&ev));
+      double tot = 0;
+      int launches = 0, rc = 0;
+      // steps queued back to back as in decode_steps (no host sync between them)
+      proj_ev_n = 0;
+      for (int i = 0; i < iters && rc == 0; ++i) rc = step_body();
+      if (rc == 0 && hipStreamSynchronize(st) != hipSuccess) rc = fail(-100, "time_stage(7): sync failed");
+      for (int j = 0; rc == 0 && j < proj_ev_n; ++j) {
+        float t = 0;
+        hipEventElapsedTime(&t, proj_ev[2 * j], proj_ev[2 * j + 1]);
+        tot += t;
+        ++launches;
+      }
+      for (auto& ev : proj_ev) hipEventDestroy(ev);
+      proj_ev.clear();
+      proj_ev_n = 0;
+      if (rc) return rc;
+      *ms = launches ? tot / launches : 0.0;
       return 0;
     } else if (what == 4) {
       // the token-selection kernel alone on the current logits (state unchanged)
