@@ -146,3 +146,23 @@ def test_sharded_replay_equals_reference(micro, run, world):
     assert [s["tokens"] for s in merged] == [s["tokens"] for s in ref]
     assert [s["seek"] for s in merged] == [s["seek"] for s in ref]
     assert [s["id"] for s in merged] == list(range(len(ref)))
+
+
+def test_time_stages(micro, window_mel):
+    """The bench's live timers (wh_time_stage): every stage returns a positive
+    per-launch time on a live beam-5 decode batch; an unknown stage fails loudly."""
+    import math
+
+    import whisper
+    from whisper.backend_hip import HipBackendError
+    from whisper.decoding import DecodingTask
+    m, _ = micro
+    m.ctx.mel_write(window_mel)
+    m.ctx.encode([0], [3000])
+    task = DecodingTask(m, whisper.DecodingOptions(language="en", beam_size=5))
+    m.ctx.decode_begin(task.wh_opts(), [task.initial_tokens], [task.sot_index])
+    for what in (0, 2, 3, 4, 5, 6, 7):
+        ms = m.ctx.time_stage(what, 2)
+        assert math.isfinite(ms) and 0.0 < ms < 100.0, (what, ms)
+    with pytest.raises(HipBackendError):
+        m.ctx.time_stage(99, 1)
