@@ -17,6 +17,10 @@
 #pragma once
 #include "wh_gemm.h"
 
+#ifndef WH_PROJ_KZ_SLOW
+#define WH_PROJ_KZ_SLOW 0
+#endif
+
 namespace wh {
 
 template <typename T, int MT, int NSUB, int KW, int NSTEP>
@@ -42,7 +46,13 @@ __global__ __launch_bounds__(64 * NSUB * KW) void k_proj(GemmArgs a) {
   const int sub = wave % NSUB, kw = wave / NSUB;
   const int nct = (a.N + P::CT - 1) / P::CT, nmg = (a.M + P::MR - 1) / P::MR, z = a.K / P::KC;
   const int bid = xcd_remap(blockIdx.x, nct * nmg * z);
+#if WH_PROJ_KZ_SLOW
+  // column tiles vary fastest: an XCD's contiguous block of logical ids shares one or
+  // two K ranges, so its X slices are fetched once into that XCD's L2 and re-read there
+  const int mg = bid % nmg, t2 = bid / nmg, ct = t2 % nct, kz = t2 / nct;
+#else
   const int mg = bid % nmg, t2 = bid / nmg, kz = t2 % z, ct = t2 / z;
+#endif
   const int kb = kz * P::KC;
   const int n0 = ct * P::CT + sub * 16, m0 = mg * P::MR;
 
