@@ -158,10 +158,26 @@ int wh_token_ms(wh_ctx* ctx, float* out, int cap, int* n, int reset);
 /* timing of the dominant kernels for roofline reporting: runs `iters` launches of
    the given stage on the context's own stream between HIP events.
    what: 0 = one decoder step graph (current batch), 1 = encoder of 1 window,
-         2 = one split-K projection GEMV launch (k_gemv_x; the six per layer, all layers),
+         2 = one split-K projection launch (k_proj; the six per layer, all layers, back to back),
          3 = one cross-attention launch (the step kernel k_cross_attn1, all layers).
-   For 2 and 3 *ms_per_iter is the average duration of a single kernel launch. */
+         4 = the token-selection kernel (k_logit_rows) on the current logits,
+         5 / 6 = 2 / 3 on layer 0 only, repeated (operands Infinity-Cache warm),
+         7 = the step's k_proj launches inside `iters` eager decoder steps, each timed by
+             its own dispatch events (advances the decode state like a step).
+   For 2, 3, 5, 6 and 7 *ms_per_iter is the average duration of a single kernel launch. */
 int wh_time_stage(wh_ctx* ctx, int what, int iters, double* ms_per_iter);
+
+/* ---- audio file decoding (host only, no context / GPU needed) ----
+   Replaces the reference's `ffmpeg` subprocess in load_audio (whisper/audio.py:42-62)
+   for FLAC input (tests/jfk.flac is 44.1 kHz stereo 24-bit).  Samples are decoded
+   bit-exactly (STREAMINFO MD5); down-mixing and resampling are done by the caller.
+   wh_flac_info: stream parameters from STREAMINFO.
+   wh_flac_decode: interleaved int32 samples [frames][channels] into out (capacity
+   cap_frames frames); *n_frames = frames decoded.  Errors: < 0, wh_flac_last_error(). */
+int wh_flac_info(const uint8_t* data, int64_t n, int* sample_rate, int* channels, int* bits_per_sample,
+                 int64_t* total_samples);
+int wh_flac_decode(const uint8_t* data, int64_t n, int32_t* out, int64_t cap_frames, int64_t* n_frames);
+const char* wh_flac_last_error(void);
 
 #ifdef __cplusplus
 }

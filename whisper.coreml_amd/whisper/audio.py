@@ -26,18 +26,38 @@ TOKENS_PER_SECOND = SAMPLE_RATE // N_SAMPLES_PER_TOKEN  # 50
 
 
 def load_audio(file: str, sr: int = SAMPLE_RATE) -> np.ndarray:
-    """Mono float32 waveform.  The reference shells out to ffmpeg (audio.py:25-62),
-    which neither this image nor the GPU box has; 16-bit PCM WAV at ``sr`` is
-    read natively, anything else needs a pre-decoded array."""
-    if not file.lower().endswith(".wav"):
-        raise RuntimeError(f"Failed to load audio: {file}: only 16-bit PCM .wav is supported without ffmpeg")
-    with wave.open(file, "rb") as w:
-        if w.getsampwidth() != 2 or w.getframerate() != sr:
-            raise RuntimeError(f"Failed to load audio: {file}: need 16-bit PCM at {sr} Hz")
-        data = np.frombuffer(w.readframes(w.getnframes()), np.int16)
-        if w.getnchannels() > 1:
-            data = data.reshape(-1, w.getnchannels()).mean(axis=1)
-    return data.astype(np.float32) / 32768.0
+    """Mono float32 waveform at ``sr`` (audio.py:25-62).  The reference pipes the file
+    through the ffmpeg CLI (``-ac 1 -ar sr -f s16le``), which neither this image nor
+    the GPU box has.  Here: FLAC is decoded by the library's host FLAC reader
+    (bit-exact, ``wh_flac_decode``) and 16-bit PCM WAV by ``wave``; then, as ffmpeg's
+    command line asks, channels are averaged to mono, the rate is converted to ``sr``
+    (polyphase FIR, ``scipy.signal.resample_poly``) and the result is quantised to
+    16-bit PCM and scaled by 1/32768.  ffmpeg's own resampling filter is not
+    reproduced, so samples differ from the reference's in the low bits wherever the
+    file's rate is not ``sr`` (parity unpinned there; exact for 16-bit files at ``sr``)."""
+    low = file.lower()
+    if low.endswith(".flac"):
+        from .backend_hip import decode_flac
+        with open(file, "rb") as f:
+            pcm, rate, bps = decode_flac(f.read())
+        x = pcm.astype(np.float64) / float(1 << (bps - 1))
+    elif low.endswith(".wav"):
+        with wave.open(file, "rb") as w:
+            if w.getsampwidth() != 2:
+                raise RuntimeError(f"Failed to load audio: {file}: need 16-bit PCM WAV")
+            rate = w.getframerate()
+            x = np.frombuffer(w.readframes(w.getnframes()), np.int16).reshape(-1, w.getnchannels())
+            x = x.astype(np.float64) / 32768.0
+    else:
+        raise RuntimeError(f"Failed to load audio: {file}: only .flac and 16-bit PCM .wav are supported without ffmpeg")
+    x = x.mean(axis=1)
+    if rate != sr:
+        from math import gcd
+        from scipy.signal import resample_poly
+        g = gcd(int(rate), int(sr))
+        x = resample_poly(x, sr // g, rate // g)
+    pcm16 = np.clip(np.round(x * 32768.0), -32768, 32767).astype(np.int16)
+    return pcm16.astype(np.float32) / 32768.0
 
 
 def pad_or_trim(array, length: int = N_SAMPLES, *, axis: int = -1):

@@ -76,6 +76,9 @@ _EXPORTS = {
     "wh_sync": (c_int, [c_void_p]),
     "wh_time_stage": (c_int, [c_void_p, c_int, c_int, POINTER(c_double)]),
     "wh_token_ms": (c_int, [c_void_p, c_void_p, c_int, POINTER(c_int), c_int]),
+    "wh_flac_info": (c_int, [c_void_p, c_int64, POINTER(c_int), POINTER(c_int), POINTER(c_int), POINTER(c_int64)]),
+    "wh_flac_decode": (c_int, [c_void_p, c_int64, c_void_p, c_int64, POINTER(c_int64)]),
+    "wh_flac_last_error": (c_char_p, []),
 }
 
 
@@ -103,6 +106,27 @@ def load_library(path: Optional[str] = None):
 
 def _ptr(a: np.ndarray):
     return a.ctypes.data_as(c_void_p)
+
+
+def decode_flac(data: bytes):
+    """FLAC bytes -> (int32 samples [frames][channels], sample_rate, bits_per_sample),
+    decoded by the library's host FLAC reader (wh_flac_decode; bit-exact)."""
+    lib = load_library()
+    buf = np.frombuffer(data, np.uint8)
+    rate, ch, bps, total = c_int(), c_int(), c_int(), c_int64()
+    rc = lib.wh_flac_info(_ptr(buf), len(buf), ctypes.byref(rate), ctypes.byref(ch), ctypes.byref(bps),
+                          ctypes.byref(total))
+    if rc != 0:
+        raise HipBackendError(f"wh_flac_info failed ({rc}): {lib.wh_flac_last_error().decode(errors='replace')}")
+    # STREAMINFO may leave the total unknown (0): size the output from the byte count
+    # (a FLAC frame cannot carry more samples than a 1-bit-per-sample verbatim one)
+    cap = total.value if total.value > 0 else len(buf) * 8
+    out = np.empty((cap, ch.value), np.int32)
+    n = c_int64()
+    rc = lib.wh_flac_decode(_ptr(buf), len(buf), _ptr(out), cap, ctypes.byref(n))
+    if rc != 0:
+        raise HipBackendError(f"wh_flac_decode failed ({rc}): {lib.wh_flac_last_error().decode(errors='replace')}")
+    return out[: n.value], rate.value, bps.value
 
 
 class DeviceAudio:
