@@ -99,8 +99,9 @@ class DecodingTask:
         return o
 
     def _text_ids(self, v) -> List[int]:
+        """decoding.py:617-619, 628-630: text is encoded as " " + text.strip()."""
         if isinstance(v, str):
-            raise NotImplementedError("text prompts/prefixes need a BPE encoder; pass token ids")
+            return self.tokenizer.encode(" " + v.strip())
         return list(v)
 
     def _initial_tokens(self, prompt) -> Tuple[int, ...]:

@@ -4,9 +4,14 @@ The hot path needs only ids: special tokens (laid out after the base BPE ranks
 exactly as ``get_encoding`` does, tokenizer.py:331-363), the SuppressTokens
 ``-1`` set (``non_speech_tokens``, tokenizer.py:253-284) and ``encode(" ")``.
 Those facts ship as data in assets/specials.json (exported from the reference
-tokenizer by oracle/gen_golden.py).  Text decoding needs the BPE rank file
+tokenizer by oracle/gen_golden.py).  Text needs the BPE rank file
 (``multilingual.tiktoken`` / ``gpt2.tiktoken``); point WHISPER_TIKTOKEN_DIR at a
-directory holding it to enable ``decode``; without it ``decode`` returns "".
+directory holding it (the tests use tests/golden/) to enable ``decode`` and
+``encode``; without it ``decode`` returns "" and ``encode`` raises.  ``encode`` is
+tiktoken's byte-level BPE restated (tiktoken is a Rust dependency of the reference,
+unpinned in requirements.txt; tokenizer.py:331-363 builds the Encoding): the text is
+split by the encoding's regex, each piece's UTF-8 bytes are merged pairwise, lowest
+merged rank first, until no adjacent pair is a token.
 """
 
 import base64
@@ -63,6 +68,35 @@ def _rank_file(name: str) -> Optional[Dict[int, bytes]]:
                 tok, rank = line.split()
                 out[int(rank)] = base64.b64decode(tok)
     return out
+
+
+# tokenizer.py:345-346 (both encodings use the GPT-2 split pattern)
+_PAT = r"""'s|'t|'re|'ve|'m|'ll|'d| ?\p{L}+| ?\p{N}+| ?[^\s\p{L}\p{N}]+|\s+(?!\S)|\s+"""
+
+
+@lru_cache(maxsize=None)
+def _encoder(name: str):
+    ranks = _rank_file(name)
+    if ranks is None:
+        return None
+    import regex
+    return {b: r for r, b in ranks.items()}, regex.compile(_PAT)
+
+
+def _bpe(piece: bytes, rank: Dict[bytes, int]) -> List[int]:
+    if piece in rank:
+        return [rank[piece]]
+    parts = [piece[i:i + 1] for i in range(len(piece))]
+    while len(parts) > 1:
+        best, bi = None, -1
+        for i in range(len(parts) - 1):
+            r = rank.get(parts[i] + parts[i + 1])
+            if r is not None and (best is None or r < best):
+                best, bi = r, i
+        if bi < 0:
+            break
+        parts[bi:bi + 2] = [parts[bi] + parts[bi + 1]]
+    return [rank[p] for p in parts]
 
 
 @dataclass
@@ -163,6 +197,18 @@ class Tokenizer:
         """True when decode(tokens).strip() == "" (transcribe.py:494-499)."""
         ws = set(self._v["whitespace_tokens"])
         return all(t in ws for t in tokens if t < self.eot)
+
+    def encode(self, text: str) -> List[int]:
+        """tokenizer.py:148-149 (``encoding.encode(text)``: plain text, no specials)."""
+        enc = _encoder(self.encoding_name)
+        if enc is None:
+            raise RuntimeError("encode needs the BPE rank file: set WHISPER_TIKTOKEN_DIR to a directory holding "
+                               f"{self.encoding_name}.tiktoken")
+        rank, pat = enc
+        out: List[int] = []
+        for piece in pat.findall(text):
+            out.extend(_bpe(piece.encode("utf-8"), rank))
+        return out
 
     def decode(self, token_ids: List[int]) -> str:
         ranks = _ranks(self.encoding_name)

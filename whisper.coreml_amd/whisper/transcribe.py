@@ -215,9 +215,10 @@ def transcribe(model: "Whisper", audio: Union[str, np.ndarray], *, verbose: Opti
     input_stride = N_FRAMES // model.dims.n_audio_ctx
     time_precision = input_stride * HOP_LENGTH / SAMPLE_RATE
 
-    if isinstance(initial_prompt, str):
-        raise NotImplementedError("text initial_prompt needs a BPE encoder; pass a list of token ids")
-    initial_prompt_tokens = list(initial_prompt) if initial_prompt else []
+    if isinstance(initial_prompt, str):  # transcribe.py:243-244
+        initial_prompt_tokens = tokenizer.encode(" " + initial_prompt.strip())
+    else:
+        initial_prompt_tokens = list(initial_prompt) if initial_prompt else []
 
     if word_timestamps and task == "translate":
         warnings.warn("Word-level timestamps on translations may not be reliable.")
