@@ -8,6 +8,8 @@
 //   PyTorchInference.rearrange_kv_cache                   (decoding.py:189-204) -> index indirection
 // k_logit_rows: one 1024-thread workgroup per decoder row (row held in registers).
 // k_merge     : one workgroup per window (candidate merge, history/ancestry update).
+#include <cstdlib>
+
 #include "wh_kernels.h"
 
 namespace wh {
@@ -292,7 +294,263 @@ __global__ __launch_bounds__(LR_THREADS) void k_logit_rows(float* __restrict__ l
   }
 }
 
+// ---------------------------------------------------------------- split selection
+// The same selection with each row's vocabulary in LP_SLICES slices, one 512-thread
+// workgroup per (row, slice): slices 0..LP_SLICES-2 split the text ids [0, ts_begin),
+// the last one is the timestamp range [ts_begin, V) on its own, so the
+// ApplyTimestampRules tail (decoding.py:522-531: logsumexp over timestamps vs the text
+// maximum) and the masking of text it may decide are both per-slice facts the combine
+// selects between.  k_logit_part applies the filters in place and writes, per slice:
+// max, sum of exp(x - max), argbest, Gumbel best, top-(G+1); k_logit_combine (one wave
+// per row) merges the kept slices.  Same choices as k_logit_rows; the normaliser is
+// summed per slice (float rounding of the log-probabilities differs in the last bits).
+constexpr int LP_THREADS = 512;
+constexpr int LP_EPT = 16;  // elements per lane: 512 x 16 >= every slice
+
+struct LPRec {
+  float mx, se, bv, gv, gx;
+  int bi, gi, pad;
+  float tv[KC];
+  int ti[KC];
+  float tail[LP_REC - 8 - 2 * KC];  // records are LP_REC words apart in s.lpart
+};
+static_assert(sizeof(LPRec) == LP_REC * 4, "slice record stride");
+
+__device__ __forceinline__ void lp_slice(int j, int tb, int V, int& lo, int& hi) {
+  if (j == LP_SLICES - 1) { lo = tb; hi = V; return; }
+  lo = (int)((int64_t)tb * j / (LP_SLICES - 1));
+  hi = (int)((int64_t)tb * (j + 1) / (LP_SLICES - 1));
+}
+
+__global__ __launch_bounds__(LP_THREADS) void k_logit_part(float* __restrict__ logits, int ldl, DecState s,
+                                                           DecOpts o) {
+  __shared__ BlockRed sm;
+  __shared__ int info[4];
+  __shared__ int pmax_w[LP_THREADS / 64];
+  const int r = blockIdx.x, j = blockIdx.y, w = r / s.G;
+  const int tid = threadIdx.x;
+  if (s.done[w]) return;
+  const int len = s.len[w], sb = s.sample_begin[w];
+  const int* hist = s.hist + (int64_t)r * s.hctx;
+  const int V = o.V, tb = o.ts_begin;
+  {  // last timestamp token of the sampled part (decoding.py:503-508)
+    int pm = -1;
+    for (int p = sb + tid; p < len; p += LP_THREADS)
+      if (hist[p] >= tb) pm = p;
+#pragma unroll
+    for (int o2 = 32; o2 > 0; o2 >>= 1) pm = max(pm, __shfl_xor(pm, o2, 64));
+    if ((tid & 63) == 0) pmax_w[tid >> 6] = pm;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    const int nseq = len - sb;
+    int pm = -1;
+    for (int k = 0; k < LP_THREADS / 64; ++k) pm = max(pm, pmax_w[k]);
+    info[0] = nseq >= 1 && hist[len - 1] >= tb;
+    info[1] = nseq < 2 || hist[len - 2] >= tb;
+    info[2] = pm >= 0 ? hist[pm] : -1;
+    info[3] = (len == sb);
+  }
+  __syncthreads();
+  const int last_ts = info[0], penult_ts = info[1], ts_last = info[2], first = info[3];
+  int mlo[4], mhi[4];
+  int nm = 0;
+  if (o.timestamps) {
+    if (last_ts) {
+      if (penult_ts) { mlo[nm] = tb; mhi[nm++] = V; }
+      else { mlo[nm] = 0; mhi[nm++] = o.eot; }
+    }
+    if (ts_last >= 0) {
+      mlo[nm] = tb;
+      mhi[nm++] = (last_ts && !penult_ts) ? ts_last : ts_last + 1;
+    }
+    if (first) {
+      mlo[nm] = 0; mhi[nm++] = tb;
+      if (o.max_initial >= 0) { mlo[nm] = tb + o.max_initial + 1; mhi[nm++] = V; }
+    }
+  }
+  const bool sb_first = first && o.suppress_blank;
+  int lo, hi;
+  lp_slice(j, tb, V, lo, hi);
+  float* row = logits + (int64_t)r * ldl;
+  float xv[LP_EPT];
+  unsigned sw[LP_EPT];
+#pragma unroll
+  for (int u = 0; u < LP_EPT; ++u) {
+    const int i = lo + tid + LP_THREADS * u;
+    xv[u] = i < hi ? row[i] : -INFINITY;
+    sw[u] = (o.suppress && i < hi) ? o.suppress[i >> 5] : 0u;
+  }
+  float mx = -INFINITY;
+#pragma unroll
+  for (int u = 0; u < LP_EPT; ++u) {
+    const int i = lo + tid + LP_THREADS * u;
+    if (i >= hi) continue;
+    bool kill = (sw[u] >> (i & 31)) & 1u;
+    if (sb_first)
+      for (int b = 0; b < o.n_blank; ++b) kill |= (i == o.blank[b]);
+    if (o.timestamps) {
+      kill |= (i == o.no_ts);
+      for (int q = 0; q < nm; ++q) kill |= (i >= mlo[q] && i < mhi[q]);
+    }
+    if (kill) {
+      xv[u] = -INFINITY;
+      row[i] = -INFINITY;
+    }
+    mx = fmaxf(mx, xv[u]);
+  }
+  mx = block_max(mx, sm);
+  LPRec* rec = reinterpret_cast<LPRec*>(s.lpart + ((int64_t)r * LP_SLICES + j) * LP_REC);
+  float se = 0.f;
+  if (mx > -INFINITY) {
+#pragma unroll
+    for (int u = 0; u < LP_EPT; ++u)
+      if (lo + tid + LP_THREADS * u < hi) se += __expf(xv[u] - mx);
+  }
+  se = block_sum(se, sm);
+  if (!o.beam) {
+    float bv = -INFINITY, gv = -INFINITY, gx = -INFINITY;
+    int bi = 0x7fffffff, gi = 0x7fffffff;
+    const unsigned long long key = splitmix64(o.seed ^ ((unsigned long long)r << 40) ^ ((unsigned long long)len << 20));
+#pragma unroll
+    for (int u = 0; u < LP_EPT; ++u) {
+      const int i = lo + tid + LP_THREADS * u;
+      if (i >= hi) continue;
+      const float x = xv[u];
+      if (better(x, i, bv, bi)) { bv = x; bi = i; }
+      if (o.temperature > 0.f && x != -INFINITY) {
+        const unsigned long long z = splitmix64(key + (unsigned long long)i);
+        const float uu = ((float)(z >> 40) + 0.5f) * (1.0f / 16777216.0f);
+        const float gsc = x / o.temperature - logf(-logf(uu));
+        if (better(gsc, i, gv, gi)) { gv = gsc; gi = i; gx = x; }
+      }
+    }
+    block_argbest(bv, bi, sm);
+    const int mine = gi;
+    const float myx = gx;
+    block_argbest(gv, gi, sm);
+    __shared__ float gx_s;
+    if (mine == gi && gi != 0x7fffffff) gx_s = myx;
+    __syncthreads();
+    if (tid == 0) {
+      rec->mx = mx; rec->se = se; rec->bv = bv; rec->bi = bi;
+      rec->gv = gv; rec->gi = gi; rec->gx = gi != 0x7fffffff ? gx_s : -INFINITY;
+    }
+    return;
+  }
+  // beam: the slice's top-(G+1) by (value desc, index asc): per-lane insertion lists,
+  // then need block-wide argbest rounds
+  const int need = s.G + 1;
+  float lv[KC];
+  int li[KC];
+#pragma unroll
+  for (int q = 0; q < KC; ++q) { lv[q] = -INFINITY; li[q] = 0x7fffffff; }
+#pragma unroll
+  for (int u = 0; u < LP_EPT; ++u) {
+    const int i = lo + tid + LP_THREADS * u;
+    if (i >= hi) continue;
+    float v = xv[u];
+    int vi = i;
+#pragma unroll
+    for (int q = 0; q < KC; ++q) {
+      if (q < need && better(v, vi, lv[q], li[q])) {
+        const float tv = lv[q]; const int ti = li[q];
+        lv[q] = v; li[q] = vi; v = tv; vi = ti;
+      }
+    }
+  }
+  int head = 0;
+  for (int q = 0; q < need; ++q) {
+    float hv = -INFINITY;
+    int hix = 0x7fffffff;
+#pragma unroll
+    for (int z = 0; z < KC; ++z)
+      if (z == head) { hv = lv[z]; hix = li[z]; }
+    float bv = hv;
+    int bi = hix;
+    block_argbest(bv, bi, sm);
+    if (bi == hix && bi != 0x7fffffff) ++head;
+    if (tid == 0) { rec->tv[q] = bv; rec->ti[q] = bi; }
+  }
+  if (tid == 0) { rec->mx = mx; rec->se = se; }
+}
+
+__global__ __launch_bounds__(64) void k_logit_combine(DecState s, DecOpts o) {
+  const int r = blockIdx.x, w = r / s.G, lane = threadIdx.x;
+  if (s.done[w]) return;
+  const LPRec* rec = reinterpret_cast<const LPRec*>(s.lpart + (int64_t)r * LP_SLICES * LP_REC);
+  constexpr int TS = LP_SLICES - 1;
+  float m = -INFINITY;
+  for (int j = 0; j < LP_SLICES; ++j) m = fmaxf(m, rec[j].mx);
+  bool text_killed = false;
+  if (o.timestamps) {
+    float st0 = 0.f, mx_tx = -INFINITY;
+    for (int j = 0; j < LP_SLICES; ++j)
+      if (rec[j].mx > -INFINITY) st0 += rec[j].se * __expf(rec[j].mx - m);
+    for (int j = 0; j < TS; ++j) mx_tx = fmaxf(mx_tx, rec[j].mx);
+    const float lS0 = logf(st0), mx_ts = rec[TS].mx;
+    const float mts = mx_ts > -INFINITY ? (mx_ts - m) - lS0 : -INFINITY;
+    const float mtx = mx_tx > -INFINITY ? (mx_tx - m) - lS0 : -INFINITY;
+    // sum over timestamps of exp(logprob - mts) = the timestamp slice's own sum
+    const float ts_lp = mts > -INFINITY ? mts + logf(rec[TS].se) : -INFINITY;
+    text_killed = ts_lp > mtx;
+    if (text_killed) m = mx_ts;
+  }
+  const int j0 = text_killed ? TS : 0;
+  float se = 0.f;
+  for (int j = j0; j < LP_SLICES; ++j)
+    if (rec[j].mx > -INFINITY) se += rec[j].se * __expf(rec[j].mx - m);
+  const float logS = logf(se);
+  float* cv = s.cand_val + (int64_t)r * KC;
+  int* ci = s.cand_idx + (int64_t)r * KC;
+  if (!o.beam) {
+    if (lane != 0) return;
+    float bv = -INFINITY, bx = -INFINITY;
+    int bi = 0x7fffffff;
+    for (int j = j0; j < LP_SLICES; ++j) {
+      if (o.temperature > 0.f) {
+        if (better(rec[j].gv, rec[j].gi, bv, bi)) { bv = rec[j].gv; bi = rec[j].gi; bx = rec[j].gx; }
+      } else if (better(rec[j].bv, rec[j].bi, bv, bi)) {
+        bv = rec[j].bv; bi = rec[j].bi; bx = rec[j].bv;
+      }
+    }
+    if (bi != 0x7fffffff) {
+      ci[0] = bi;
+      cv[0] = (bx - m) - logS;
+    }
+    return;
+  }
+  // merge the kept slices' sorted top lists (lane 0; at most 8 x 9 candidates)
+  if (lane != 0) return;
+  const int need = s.G + 1;
+  int hd[LP_SLICES];
+  for (int j = 0; j < LP_SLICES; ++j) hd[j] = 0;
+  for (int q = 0; q < need; ++q) {
+    float bv = -INFINITY;
+    int bi = 0x7fffffff, bj = -1;
+    for (int j = j0; j < LP_SLICES; ++j)
+      if (hd[j] < need && better(rec[j].tv[hd[j]], rec[j].ti[hd[j]], bv, bi)) {
+        bv = rec[j].tv[hd[j]]; bi = rec[j].ti[hd[j]]; bj = j;
+      }
+    if (bj >= 0 && bi != 0x7fffffff) ++hd[bj];
+    cv[q] = (bv - m) - logS;
+    ci[q] = bi;
+  }
+}
+
 void launch_logit_rows(float* logits, int ldl, const DecState& s, const DecOpts& o, int nwin, hipStream_t st) {
+  // the sliced selection (k_logit_part + k_logit_combine) unless WHISPER_HIP_LOGIT_SPLIT=0
+  // (config 2, turbo one window: 0.380 -> 0.346 ms per token; config 3 unchanged)
+  static const bool split = [] {
+    const char* e = getenv("WHISPER_HIP_LOGIT_SPLIT");
+    return !(e && e[0] == '0');
+  }();
+  const int slice_max = (o.ts_begin + LP_SLICES - 2) / (LP_SLICES - 1);
+  if (split && slice_max <= LP_THREADS * LP_EPT && o.V - o.ts_begin <= LP_THREADS * LP_EPT && o.ts_begin > 0) {
+    k_logit_part<<<dim3(nwin * s.G, LP_SLICES), LP_THREADS, 0, st>>>(logits, ldl, s, o);
+    k_logit_combine<<<nwin * s.G, 64, 0, st>>>(s, o);
+    return;
+  }
   k_logit_rows<<<nwin * s.G, LR_THREADS, 0, st>>>(logits, ldl, s, o);
 }
 

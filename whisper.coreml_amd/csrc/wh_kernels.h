@@ -72,6 +72,7 @@ struct DecState {
   int* fin_tok;      // [nw][maxc][hctx]
   float* cand_val;   // [nw*G][KC]
   int* cand_idx;     // [nw*G][KC]
+  float* lpart;      // [nw*G][LP_SLICES][LP_REC] per-slice token-selection partials
   int nw, G, ctx, hctx, maxc;
 };
 
@@ -88,6 +89,8 @@ struct DecOpts {
   unsigned long long seed;
 };
 
+constexpr int LP_SLICES = 8;  // vocabulary slices per row: 7 text slices + [timestamp_begin, V)
+constexpr int LP_REC = 32;    // words per slice record
 void launch_logit_rows(float* logits, int ldl, const DecState& s, const DecOpts& o, int nwin, hipStream_t st);
 void launch_merge(const DecState& s, const DecOpts& o, int nwin, hipStream_t st);
 void launch_no_speech(const float* logits, int ldl, int rows, int V, int no_speech, float* out, hipStream_t st);

@@ -307,6 +307,7 @@ struct Ctx : public wh_ctx {
     addA(Wcap * Gcap * 4);
     addA(Wcap * 16 * 4); addA(Wcap * 16 * 4); addA((size_t)Wcap * 16 * HCTX * 4);
     addA((size_t)Wcap * Gcap * KC * 4); addA((size_t)Wcap * Gcap * KC * 4);
+    addA((size_t)Wcap * Gcap * LP_SLICES * LP_REC * 4);
     addA(64);
     HIPCHK(hipMalloc(&abase, ab));
     HIPCHK(hipMemset(abase, 0, ab));
@@ -338,6 +339,7 @@ struct Ctx : public wh_ctx {
     S.sum_lp = fa(Wcap * Gcap);
     S.fin_score = fa(Wcap * 16); S.fin_len = ia(Wcap * 16); S.fin_tok = ia((size_t)Wcap * 16 * HCTX);
     S.cand_val = fa((size_t)Wcap * Gcap * KC); S.cand_idx = ia((size_t)Wcap * Gcap * KC);
+    S.lpart = fa((size_t)Wcap * Gcap * LP_SLICES * LP_REC);
     if (!S.cand_idx) return fail(-3, "activation arena overflow");
     S.nw = Wcap; S.G = 1; S.ctx = CTX; S.hctx = HCTX; S.maxc = 16;
     HIPCHK(hipMalloc(&d_gmax, 64));
