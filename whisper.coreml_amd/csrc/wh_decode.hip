@@ -6,7 +6,10 @@
 //   GreedyDecoder.update                                  (decoding.py:304-320)
 //   BeamSearchDecoder.update incl. finished bookkeeping   (decoding.py:350-409)
 //   PyTorchInference.rearrange_kv_cache                   (decoding.py:189-204) -> index indirection
-// k_logit_rows: one 1024-thread workgroup per decoder row (row held in registers).
+// k_logit_part + k_logit_combine (default): 8 vocabulary slices per row, one workgroup
+//               each, then one wave per row merging the kept slices.
+// k_logit_rows: the single-workgroup form (one 1024-thread workgroup per decoder row;
+//               WHISPER_HIP_LOGIT_SPLIT=0).
 // k_merge     : one workgroup per window (candidate merge, history/ancestry update).
 #include <cstdlib>
 
