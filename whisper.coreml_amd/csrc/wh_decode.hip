@@ -481,7 +481,16 @@ __global__ __launch_bounds__(LP_THREADS) void k_logit_part(float* __restrict__ l
 __global__ __launch_bounds__(64) void k_logit_combine(DecState s, DecOpts o) {
   const int r = blockIdx.x, w = r / s.G, lane = threadIdx.x;
   if (s.done[w]) return;
-  const LPRec* rec = reinterpret_cast<const LPRec*>(s.lpart + (int64_t)r * LP_SLICES * LP_REC);
+  // the row's slice records -> LDS in one round trip (the merge below reads them
+  // serially; from global memory every read would be a dependent load)
+  __shared__ __attribute__((aligned(16))) float recs[LP_SLICES * LP_REC];
+  {
+    const float4_t* src = reinterpret_cast<const float4_t*>(s.lpart + (int64_t)r * LP_SLICES * LP_REC);
+    float4_t* dst = reinterpret_cast<float4_t*>(recs);
+    for (int k = lane; k < LP_SLICES * LP_REC / 4; k += 64) dst[k] = src[k];
+  }
+  __syncthreads();
+  const LPRec* rec = reinterpret_cast<const LPRec*>(recs);
   constexpr int TS = LP_SLICES - 1;
   float m = -INFINITY;
   for (int j = 0; j < LP_SLICES; ++j) m = fmaxf(m, rec[j].mx);
