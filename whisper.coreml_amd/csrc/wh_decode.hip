@@ -308,6 +308,12 @@ __global__ __launch_bounds__(LR_THREADS) void k_logit_rows(float* __restrict__ l
 // per row) merges the kept slices.  Same choices as k_logit_rows; the normaliser is
 // summed per slice (float rounding of the log-probabilities differs in the last bits).
 constexpr int LP_THREADS = 512;
+// WH_LP_OCC=1: cap k_logit_part at 80 VGPRs (6 waves per SIMD: 3 workgroups per CU)
+#if defined(WH_LP_OCC) && WH_LP_OCC
+#define WH_LP_ATTR __attribute__((amdgpu_waves_per_eu(6, 8)))
+#else
+#define WH_LP_ATTR
+#endif
 constexpr int LP_EPT = 16;  // elements per lane: 512 x 16 >= every slice
 
 struct LPRec {
@@ -325,7 +331,7 @@ __device__ __forceinline__ void lp_slice(int j, int tb, int V, int& lo, int& hi)
   hi = (int)((int64_t)tb * (j + 1) / (LP_SLICES - 1));
 }
 
-__global__ __launch_bounds__(LP_THREADS) void k_logit_part(float* __restrict__ logits, int ldl, DecState s,
+__global__ __launch_bounds__(LP_THREADS) WH_LP_ATTR void k_logit_part(float* __restrict__ logits, int ldl, DecState s,
                                                            DecOpts o) {
   __shared__ BlockRed sm;
   __shared__ int info[4];
