@@ -18,6 +18,11 @@
  *           beam/filter loop (whisper/decoding.py:707-737)
  *        -> wh_decode_steps (one hipGraph per token: decoder step, logit filters,
  *           greedy/beam update, KV reorder by index indirection)
+ *   the same roles one call per token, for a caller that keeps the reference's
+ *   host loop (PyTorchInference.logits / rearrange_kv_cache, decoding.py:151-204):
+ *        decoder256Predict (coreml.h:15-21) -> wh_prefill
+ *        decoder1Predict   (coreml.h:26-31) -> wh_step
+ *        rearrange_mkv     (coreml.h:25)    -> wh_reorder_kv
  *   log_mel_spectrogram (whisper/audio.py:110-157) -> wh_log_mel
  *   showCoremlPredictTime (whisper/coreml.py:247-263) -> wh_stats
  *
@@ -60,6 +65,8 @@ typedef struct wh_decode_opts {
   const int* suppress;   /* SuppressTokens ids (already resolved, -1 expanded) */
   int n_suppress;
   unsigned long long seed; /* sampling RNG seed */
+  int max_candidates;    /* beam: round(beam_size * patience) as the host computes it
+                            (Python round, decoding.py:339); <= 0: derived from patience */
 } wh_decode_opts;
 
 const char* wh_last_error(void);
@@ -106,6 +113,12 @@ int wh_read_cross_kv(wh_ctx* ctx, int slot, int layer, float* k_out, float* v_ou
    (init_tokens[w*max_init + i], i < n_init[w]) and the first token update */
 int wh_decode_begin(wh_ctx* ctx, int n_win, const wh_decode_opts* opts, const int* init_tokens, const int* n_init,
                     int max_init, const int* sot_index);
+/* wh_decode_begin where decode window w attends to the audio features of encoder slot
+   slots[w] (the temperature fallback, transcribe.py:188-228, re-decodes only the
+   windows that failed, from the slots that already hold them).  wh_decode_read's
+   `slot` is the decode window index w. */
+int wh_decode_begin_slots(wh_ctx* ctx, int n_win, const int* slots, const wh_decode_opts* opts,
+                          const int* init_tokens, const int* n_init, int max_init, const int* sot_index);
 /* run up to max_steps token updates (hipGraph); *n_done = windows finished */
 int wh_decode_steps(wh_ctx* ctx, int max_steps, int* n_done);
 /* read back a window: tokens [group][n_text_ctx+1], sum_logprobs [group], len,
@@ -113,6 +126,27 @@ int wh_decode_steps(wh_ctx* ctx, int max_steps, int* n_done);
 int wh_decode_read(wh_ctx* ctx, int slot, int* tokens, float* sum_logprobs, int* len, int* fin_n, int* fin_tokens,
                    int* fin_len, float* fin_score, float* no_speech_prob);
 int wh_decode_maxc(wh_ctx* ctx);
+
+/* ---- per-step boundary (the reference's decoder256Predict / decoder1Predict /
+   rearrange_mkv, coreml.h:15-31, driven by its host DecodingTask loop,
+   decoding.py:707-737).  Rows are r = w * group + b for windows w < n_win (slots
+   0..n_win-1, encoded by wh_encode) and beams b < group.
+
+   wh_prefill: first pass of each window's initial tokens (tokens[w * max_tokens + i],
+   i < n_tokens[w]; all rows of a window share them, coreml.mm:279-327 runs the same
+   pass once per beam).  logits (nullable) [n_win][2][n_vocab]: the rows at position
+   sot_index[w] (no-speech probability, decoding.py:716-720) and n_tokens[w] - 1. */
+int wh_prefill(wh_ctx* ctx, int n_win, int group, const int* tokens, const int* n_tokens, int max_tokens,
+               const int* sot_index, float* logits);
+/* wh_step: one decoder step.  Row r appends tokens[r] (the token the host chose for it)
+   at position text_offsets[w] (nullable; when given it must equal the window's cached
+   length, the text_offset of decoder1Predict) and returns logits [n_win*group][n_vocab]
+   (nullable: kept on the device only). */
+int wh_step(wh_ctx* ctx, const int* tokens, const int* text_offsets, float* logits);
+/* wh_reorder_kv: after a beam update, row r continues the sequence of row
+   source_rows[r] (a row of the same window; PyTorchInference.rearrange_kv_cache).
+   No cache bytes move: the rows' ancestry tables are permuted.  Once per step. */
+int wh_reorder_kv(wh_ctx* ctx, const int* source_rows);
 
 /* decoder forward over tokens at offset 0 for one window slot (Whisper.forward,
    model.py:110-119 / the decoder256 first pass); logits [n_tokens][n_vocab];

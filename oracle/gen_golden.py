@@ -84,6 +84,80 @@ class MarginRecorder:
         ref_decoding.GreedyDecoder.update = self._orig
 
 
+class StepRecorder:
+    """Wraps PyTorchInference.logits / rearrange_kv_cache (decoding.py:151-204) to record,
+    for every decoder call of the reference's _main_loop (decoding.py:707-737): the last
+    input token of each row, the top-K of the raw last-position logits (before the logit
+    filters modify them in place, decoding.py:726-727) with the row's logsumexp, and the
+    beam reorder indices.  This is the trajectory a teacher-forced step replays."""
+
+    def __init__(self, k: int = 32):
+        self.tok, self.topv, self.topi, self.lse, self.src = [], [], [], [], []
+        self._orig = (ref_decoding.PyTorchInference.logits, ref_decoding.PyTorchInference.rearrange_kv_cache)
+        rec, orig_logits, orig_rearr = self, self._orig[0], self._orig[1]
+
+        def logits(this, tokens, audio_features):
+            out, qk = orig_logits(this, tokens, audio_features)
+            last = out[:, -1].detach().float().clone()
+            v, i = torch.topk(last, k, dim=-1)
+            rec.tok.append(tokens[:, -1].tolist())
+            rec.topv.append(v.numpy())
+            rec.topi.append(i.numpy())
+            rec.lse.append(torch.logsumexp(last.double(), dim=-1).numpy())
+            return out, qk
+
+        def rearrange(this, source_indices):
+            rec.src.append(list(source_indices))
+            return orig_rearr(this, source_indices)
+
+        ref_decoding.PyTorchInference.logits = logits
+        ref_decoding.PyTorchInference.rearrange_kv_cache = rearrange
+
+    def close(self):
+        ref_decoding.PyTorchInference.logits, ref_decoding.PyTorchInference.rearrange_kv_cache = self._orig
+
+    def pack(self, prefix: str, out: dict):
+        out[f"{prefix}_tok"] = np.asarray(self.tok, dtype=np.int32)          # [steps][rows]
+        out[f"{prefix}_topv"] = np.stack(self.topv).astype(np.float32)       # [steps][rows][K]
+        out[f"{prefix}_topi"] = np.stack(self.topi).astype(np.int32)
+        out[f"{prefix}_lse"] = np.stack(self.lse).astype(np.float64)         # [steps][rows]
+        if self.src:
+            out[f"{prefix}_src"] = np.asarray(self.src, dtype=np.int32)      # [steps][rows]
+
+
+def step_goldens(name: str, seed: int = 0, audio_seed: int = 1, mixed_seeds=(2, 3, 4)):
+    """Per-step reference trajectories for the fp16/beam tolerance test (teacher-forced
+    steps through wh_step / wh_reorder_kv) and fixed-work tokens of further windows for
+    the co-batched (bench-configuration) parity test."""
+    t0 = time.time()
+    model, _ = build_ref_model(name, seed)
+    dims = syn.MODEL_DIMS[name]
+    eot = 50257 if dims["n_vocab"] >= 51865 else 50256
+    out = {"seed": np.int32(seed), "audio_seed": np.int32(audio_seed), "mixed_seeds": np.asarray(mixed_seeds, np.int32)}
+
+    def window(aseed):
+        audio = syn.synthetic_audio(30.0, seed=aseed)
+        mel = ref_audio.log_mel_spectrogram(audio, dims["n_mels"], padding=N_SAMPLES)
+        return ref_audio.pad_or_trim(mel[:, :3000], 3000)
+
+    seg = window(audio_seed)
+    for kind, extra in [("greedy_fixed", {}), ("beam_fixed", dict(beam_size=5))]:
+        rec = StepRecorder()
+        r = refw.decode(model, seg, ref_decoding.DecodingOptions(
+            temperature=0.0, suppress_tokens=f"-1,{eot}", language="en", fp16=False, **extra))
+        rec.close()
+        rec.pack(f"tf_{kind}", out)
+        out[f"tf_{kind}_tokens"] = np.asarray(r.tokens, dtype=np.int32)
+        print(f"[{name}] steps {kind}: {len(rec.tok)} calls {time.time()-t0:.1f}s", flush=True)
+    for s in mixed_seeds:
+        seg = window(s)
+        r = refw.decode(model, seg, ref_decoding.DecodingOptions(
+            temperature=0.0, beam_size=5, suppress_tokens=f"-1,{eot}", language="en", fp16=False))
+        pack_result(f"mixed{s}_beam_fixed", r, out)
+        print(f"[{name}] mixed window seed {s}: {len(r.tokens)} tok {time.time()-t0:.1f}s", flush=True)
+    np.savez_compressed(os.path.join(OUT, f"{name}_steps.npz"), **out)
+
+
 def pack_result(prefix: str, r, out: dict):
     out[f"{prefix}_tokens"] = np.asarray(r.tokens, dtype=np.int32)
     out[f"{prefix}_avg_logprob"] = np.float64(r.avg_logprob)
@@ -200,7 +274,7 @@ def transcribe_goldens(model, name: str, out: dict):
         json.dump(dict(audio_seconds=65.0, audio_seed=7, runs=runs, segments=segs_all), f, indent=0)
 
 
-def words_goldens(model, name: str):
+def words_goldens(model, name: str, run_keys=None):
     """Word-level timestamps (config 5 / SURVEY §8 a19): the reference's own
     find_alignment on one window, and transcribe(word_timestamps=True) on 65 s of
     audio; plus the decoded bytes of every token id involved (the product ships no
@@ -237,6 +311,8 @@ def words_goldens(model, name: str):
         "seq_greedy_halluc": dict(condition_on_previous_text=True, word_timestamps=True,
                                   hallucination_silence_threshold=2.0),
     }
+    if run_keys is not None:
+        runs = {k: v for k, v in runs.items() if k in run_keys}
     for key, kw in runs.items():
         t0 = time.time()
         out = refw.transcribe(model, audio, temperature=0.0, language="en", fp16=False, verbose=None, **kw)
@@ -395,8 +471,14 @@ def main(argv):
         elif w == "assets":
             asset_export()
         elif w.endswith("_words"):
-            model, _ = build_ref_model(w[:-len("_words")])
-            words_goldens(model, w[:-len("_words")])
+            base = w[:-len("_words")]
+            model, _ = build_ref_model(base)
+            # full-size models: find_alignment with the real alignment heads plus one
+            # clip-grid transcribe run (the sequential and beam runs cost minutes each on CPU)
+            big = base in ("turbo", "large-v3")
+            words_goldens(model, base, run_keys=("clip_greedy_words",) if big else None)
+        elif w.endswith("_steps"):
+            step_goldens(w[:-len("_steps")])
         else:
             small = w.startswith("micro")
             big = w in ("turbo", "large-v3", "large-v3-turbo")

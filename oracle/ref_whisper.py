@@ -301,8 +301,14 @@ def apply_filters(logits: torch.Tensor, tokens: torch.Tensor, sample_begin: int,
 
 
 def decode(model: OracleWhisper, mel: torch.Tensor, opts: Options, st: Optional[SpecialTokens] = None,
-           xa: Optional[torch.Tensor] = None) -> Result:
-    """DecodingTask.run (decoding.py:740-816) for one window, temperature 0."""
+           xa: Optional[torch.Tensor] = None, inference=None) -> Result:
+    """DecodingTask.run (decoding.py:740-816) for one window, temperature 0.
+
+    ``inference`` (tests only): an object with the reference's Inference interface
+    (``logits(tokens, audio_features)``, ``rearrange_kv_cache(source_indices)``,
+    decoding.py:127-204) that replaces the oracle's own decoder calls, so this host
+    loop drives another implementation's per-step boundary (libwhisper_hip's
+    wh_prefill / wh_step / wh_reorder_kv through whisper.inference.HipInference)."""
     st = st or SpecialTokens.for_model(model.dims)
     n_text_ctx = model.dims["n_text_ctx"]
     sample_len = opts.sample_len or n_text_ctx // 2
@@ -318,9 +324,10 @@ def decode(model: OracleWhisper, mel: torch.Tensor, opts: Options, st: Optional[
     max_init = None
     if not opts.without_timestamps and opts.max_initial_timestamp:
         max_init = round(opts.max_initial_timestamp / (30.0 / model.dims["n_audio_ctx"]))
-    if xa is None:
-        xa = model.encode(mel)
-    model.set_audio(xa)
+    if inference is None:
+        if xa is None:
+            xa = model.encode(mel)
+        model.set_audio(xa)
     G = opts.beam_size or 1
     tokens = torch.tensor([init] * G)
     sum_lp = torch.zeros(G)
@@ -330,9 +337,12 @@ def decode(model: OracleWhisper, mel: torch.Tensor, opts: Options, st: Optional[
     max_cand = round(G * (opts.patience or 1.0))
     no_speech = float("nan")
     for i in range(sample_len):
-        inp = tokens if i == 0 else tokens[:, -1:]
-        logits, cache, _ = model.decoder_forward(inp, offset, cache)
-        offset += inp.shape[1]
+        if inference is None:
+            inp = tokens if i == 0 else tokens[:, -1:]
+            logits, cache, _ = model.decoder_forward(inp, offset, cache)
+            offset += inp.shape[1]
+        else:
+            logits = torch.from_numpy(np.asarray(inference.logits(tokens, None)[0]))
         if i == 0:
             no_speech = logits[:, sot_index].float().softmax(dim=-1)[0, st.no_speech].item()
         logits = logits[:, -1].clone()
@@ -365,7 +375,10 @@ def decode(model: OracleWhisper, mel: torch.Tensor, opts: Options, st: Optional[
                     if len(alive) == G:
                         break
             tokens = torch.tensor(alive)
-            cache = [[c[0][src], c[1][src]] for c in cache]
+            if inference is None:
+                cache = [[c[0][src], c[1][src]] for c in cache]
+            else:
+                inference.rearrange_kv_cache(src)
             for seq in sorted(new_fin, key=new_fin.get, reverse=True):
                 if len(finished) >= max_cand:
                     break

@@ -19,7 +19,8 @@ def _declared():
 def test_header_declares_entry_points():
     names = _declared()
     for must in ("wh_create", "wh_destroy", "wh_load_tensor", "wh_finalize", "wh_log_mel", "wh_encode",
-                 "wh_decode_begin", "wh_decode_steps", "wh_decode_read", "wh_prefill_logits", "wh_last_error"):
+                 "wh_decode_begin", "wh_decode_steps", "wh_decode_read", "wh_prefill_logits", "wh_last_error",
+                 "wh_prefill", "wh_step", "wh_reorder_kv", "wh_decode_begin_slots"):
         assert must in names
 
 
@@ -46,4 +47,11 @@ def test_create_fails_loudly_without_gpu():
     except Exception:
         pass
     with pytest.raises(whisper.HipBackendError):
-        whisper.load_model("micro", device=0)
+        whisper.load_model("micro", device=0, synthetic=True)
+
+
+def test_load_model_without_checkpoint_raises(tmp_path):
+    """No silent random weights: a missing checkpoint raises unless synthetic=True."""
+    import whisper
+    with pytest.raises(RuntimeError, match="not found"):
+        whisper.load_model("large-v3", device=0, download_root=str(tmp_path))

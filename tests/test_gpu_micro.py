@@ -21,7 +21,8 @@ def _golden(name):
 @pytest.fixture(scope="module", params=["fp32", "fp16"])
 def micro(request):
     import whisper
-    m = whisper.load_model("micro", device=0, dtype=request.param, max_windows=4, max_group=5)
+    m = whisper.load_model("micro", device=0, dtype=request.param, max_windows=4, max_group=5,
+                             synthetic=True)
     yield m, request.param
     m.close()
 
@@ -100,7 +101,7 @@ def test_decode_tokens(micro, window_mel, key, opts):
         assert agree >= 1
 
 
-@pytest.mark.parametrize("run,schedule", [("clip_beam", "auto"), ("clip_greedy", "auto"), ("seq_greedy", "auto"),
+@pytest.mark.parametrize("run,schedule", [("clip_beam", "auto"), ("clip_greedy", "auto"), ("seq_greedy", "auto"), ("seq_beam", "auto"),
                                           ("clip_beam", "sequential"), ("clip_greedy", "sequential")])
 def test_transcribe_segments(micro, run, schedule):
     """clip runs under "auto" take the batched schedule (all clips' windows through

@@ -26,34 +26,14 @@ def _golden(name):
     return np.load(os.path.join(GOLDEN, f"{name}.npz"))
 
 
-_cache = {}
-
-
 def _model(name, dtype):
-    import whisper
-    from whisper import synthetic as S
-    key = (name, dtype)
-    if key not in _cache:
-        for k in list(_cache):
-            _cache.pop(k).close()
-        g = _golden(name)
-        sd = S.synthetic_state_dict(S.MODEL_DIMS[name], int(g["seed"]))
-        assert S.state_dict_checksum(sd) == pytest.approx(float(g["weights_checksum"]), rel=1e-12)
-        m = whisper.Whisper(whisper.ModelDimensions(**S.MODEL_DIMS[name]), name, device=0, dtype=dtype,
-                            max_windows=1, max_group=5)
-        m.load_state_dict(sd)
-        del sd
-        _cache[key] = m
-    return _cache[key]
+    from conftest import full_model
+    return full_model(name, dtype)
 
 
 def _window(name):
-    import whisper
-    from whisper import synthetic as S
-    g = _golden(name)
-    audio = S.synthetic_audio(30.0, seed=int(g["audio_seed"]))
-    mel = whisper.log_mel_spectrogram(audio, S.MODEL_DIMS[name]["n_mels"], padding=whisper.audio.N_SAMPLES)
-    return whisper.pad_or_trim(mel[:, :3000], 3000)
+    from conftest import golden_window
+    return golden_window(name)
 
 
 @pytest.mark.parametrize("dtype", ["fp16", "fp32"])

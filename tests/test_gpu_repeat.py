@@ -18,7 +18,8 @@ pytestmark = pytest.mark.gpu
 @pytest.fixture(scope="module")
 def micro32():
     import whisper
-    m = whisper.load_model("micro", device=0, dtype="fp32", max_windows=4, max_group=5)
+    m = whisper.load_model("micro", device=0, dtype="fp32", max_windows=4, max_group=5,
+                             synthetic=True)
     yield m
     m.close()
 

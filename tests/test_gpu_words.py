@@ -34,7 +34,8 @@ def micro32(words_golden):
     from whisper import tokenizer as T
     enc = words_golden["encoding"].replace(".tiktoken", "")
     T.set_token_bytes(enc, {int(k): base64.b64decode(v) for k, v in words_golden["token_bytes"].items()})
-    m = whisper.load_model("micro", device=0, dtype="fp32", max_windows=4, max_group=5)
+    m = whisper.load_model("micro", device=0, dtype="fp32", max_windows=4, max_group=5,
+                             synthetic=True)
     yield m
     m.close()
     T.set_token_bytes(enc, None)
@@ -166,3 +167,53 @@ def test_align_batch_equals_single_windows(micro32, words_golden):
         np.testing.assert_allclose(batch[w][0], one[0], rtol=1e-5)
         np.testing.assert_array_equal(batch[w][1], one[1])
         np.testing.assert_array_equal(batch[w][2], one[2])
+
+
+# ---------------------------------------------------------------- large-v3 (config 5)
+@pytest.fixture(scope="module")
+def lv3_words():
+    with open(os.path.join(GOLDEN, "large-v3_words.json")) as f:
+        return json.load(f)
+
+
+def test_large_v3_find_alignment_matches_reference(lv3_words):
+    """find_alignment at large-v3 with its 10 real alignment heads
+    (/root/reference/whisper/__init__.py:51) against the reference's own output."""
+    from conftest import full_model
+    from whisper.timing import _alignment_head_ids, find_alignment
+    from whisper.tokenizer import get_tokenizer
+    m = full_model("large-v3", "fp32")
+    assert len(_alignment_head_ids(m)) == 10
+    _window0(m, lv3_words)
+    tok = get_tokenizer(m.is_multilingual, num_languages=m.num_languages, language="en", task="transcribe")
+    for key, case in lv3_words["find_alignment"].items():
+        got = find_alignment(m, tok, case["text_tokens"], case["num_frames"])
+        ref = case["words"]
+        assert [w.word for w in got] == [w["word"] for w in ref], key
+        assert [w.tokens for w in got] == [w["tokens"] for w in ref], key
+        np.testing.assert_allclose([w.start for w in got], [w["start"] for w in ref], rtol=0, atol=1e-9, err_msg=key)
+        np.testing.assert_allclose([w.end for w in got], [w["end"] for w in ref], rtol=0, atol=1e-9, err_msg=key)
+        np.testing.assert_allclose([w.probability for w in got], [w["probability"] for w in ref], rtol=2e-3,
+                                   err_msg=key)
+
+
+def test_large_v3_transcribe_word_timestamps(lv3_words):
+    """Config 5 (large-v3 --word_timestamps) on 65 s, clip grid, greedy, fp32:
+    segments and words equal the reference's transcribe()."""
+    import whisper
+    from conftest import full_model
+    from whisper import synthetic as S
+    m = full_model("large-v3", "fp32")
+    run = "clip_greedy_words"
+    kw = dict(lv3_words["runs"][run])
+    audio = S.synthetic_audio(lv3_words["audio_seconds"], seed=lv3_words["audio_seed"])
+    out = whisper.transcribe(m, audio, temperature=0.0, language="en", **kw)
+    ref = lv3_words["segments"][run]
+    assert [s["tokens"] for s in out["segments"]] == [s["tokens"] for s in ref]
+    assert [s["seek"] for s in out["segments"]] == [s["seek"] for s in ref]
+    for a, b in zip(out["segments"], ref):
+        assert a["start"] == pytest.approx(b["start"]) and a["end"] == pytest.approx(b["end"])
+        assert [w["word"] for w in a["words"]] == [w["word"] for w in b["words"]]
+        for wa, wb in zip(a["words"], b["words"]):
+            assert wa["start"] == pytest.approx(wb["start"]) and wa["end"] == pytest.approx(wb["end"])
+            assert wa["probability"] == pytest.approx(wb["probability"], rel=2e-3)

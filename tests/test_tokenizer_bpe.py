@@ -1,19 +1,17 @@
 """BPE text encoding / decoding (reference tests/test_tokenizer.py) with the rank
-files the reference's tokenizer loads (tests/golden/{gpt2,multilingual}.tiktoken,
-data copied as fixtures), and text prompts end to end (decoding.py:614-640,
-transcribe.py:243-244)."""
+files the reference's tokenizer loads ({gpt2,multilingual}.tiktoken, data the
+reference ships in whisper/assets and this package ships in whisper/assets), and
+text prompts end to end (decoding.py:614-640, transcribe.py:243-244)."""
 import os
 
 import numpy as np
 import pytest
 
-from conftest import GOLDEN
-
 
 @pytest.fixture(autouse=True)
 def bpe_tables(monkeypatch):
     from whisper import tokenizer as T
-    monkeypatch.setenv("WHISPER_TIKTOKEN_DIR", GOLDEN)
+    monkeypatch.delenv("WHISPER_TIKTOKEN_DIR", raising=False)
     T._rank_file.cache_clear()
     T._encoder.cache_clear()
     yield
@@ -68,13 +66,29 @@ def test_known_ids_and_round_trips():
     assert ml.encode(" ") == ml.encode_blank()
 
 
-def test_encode_needs_rank_file(monkeypatch):
+def test_text_needs_rank_file(monkeypatch, tmp_path):
+    """A directory without the rank files: encode and decode fail loudly (no silent "")."""
     from whisper import tokenizer as T
-    monkeypatch.delenv("WHISPER_TIKTOKEN_DIR")
+    monkeypatch.setenv("WHISPER_TIKTOKEN_DIR", str(tmp_path))
     T._rank_file.cache_clear()
     T._encoder.cache_clear()
+    tok = T.get_tokenizer(multilingual=True)
     with pytest.raises(RuntimeError):
-        T.get_tokenizer(multilingual=True).encode("x")
+        tok.encode("x")
+    with pytest.raises(RuntimeError):
+        tok.decode([400])
+
+
+def test_split_to_word_tokens_spaces_and_punctuation():
+    """split_tokens_on_spaces semantics (tokenizer.py:313-327): a piece starts a word
+    when it is special, begins with a space or is punctuation."""
+    from whisper.tokenizer import get_tokenizer
+    ml = get_tokenizer(multilingual=True, language="en")
+    ids = ml.encode(" Hello, wonderful world!") + [ml.eot]
+    words, groups = ml.split_to_word_tokens(ids)
+    assert "".join(words[:-1]) == " Hello, wonderful world!"
+    assert words[0] == " Hello" and words[1] == "," and words[-1] == "<|endoftext|>"
+    assert [t for g in groups for t in g] == ids
 
 
 @pytest.mark.gpu

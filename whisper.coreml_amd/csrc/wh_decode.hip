@@ -209,7 +209,7 @@ __global__ __launch_bounds__(LR_THREADS) void k_logit_rows(float* __restrict__ l
     float bv = -INFINITY, bx = -INFINITY;
     int bi = 0x7fffffff;
     if (o.temperature > 0.f) {
-      const unsigned long long key = splitmix64(o.seed ^ ((unsigned long long)r << 40) ^ ((unsigned long long)len << 20));
+      const unsigned long long key = splitmix64(s.seed[0] ^ ((unsigned long long)r << 40) ^ ((unsigned long long)len << 20));
       ROW_PASS(text_killed, {
         se += __expf(x - m);
         if (x != -INFINITY) {
@@ -420,7 +420,7 @@ __global__ __launch_bounds__(LP_THREADS) WH_LP_ATTR void k_logit_part(float* __r
   if (!o.beam) {
     float bv = -INFINITY, gv = -INFINITY, gx = -INFINITY;
     int bi = 0x7fffffff, gi = 0x7fffffff;
-    const unsigned long long key = splitmix64(o.seed ^ ((unsigned long long)r << 40) ^ ((unsigned long long)len << 20));
+    const unsigned long long key = splitmix64(s.seed[0] ^ ((unsigned long long)r << 40) ^ ((unsigned long long)len << 20));
 #pragma unroll
     for (int u = 0; u < LP_EPT; ++u) {
       const int i = lo + tid + LP_THREADS * u;
@@ -695,6 +695,52 @@ __global__ __launch_bounds__(256) void k_merge(DecState s, DecOpts o) {
 
 void launch_merge(const DecState& s, const DecOpts& o, int nwin, hipStream_t st) {
   k_merge<<<nwin, 256, 0, st>>>(s, o);
+}
+
+// ------------------------------------------------------------ per-step ABI state updates
+// wh_step: row r of window w takes token tok[r] at position len[w] (the token the host's
+// decoder.update chose, decoding.py:730); the step then embeds hist[len - 1].
+__global__ __launch_bounds__(64) void k_append_tokens(DecState s, const int* __restrict__ tok) {
+  const int w = blockIdx.x, b = threadIdx.x;
+  const int len = s.len[w];
+  if (b < s.G) {
+    s.hist[((int64_t)w * s.G + b) * s.hctx + len] = tok[w * s.G + b];
+    // the step writes this position's K/V into the row's own slot
+    if (len < s.ctx) s.anc[((int64_t)w * s.G + b) * s.ctx + len] = b;
+  }
+  __syncthreads();
+  if (b == 0) s.len[w] = len + 1;
+}
+void launch_append_tokens(const DecState& s, const int* tok, int nwin, hipStream_t st) {
+  k_append_tokens<<<nwin, 64, 0, st>>>(s, tok);
+}
+
+// wh_reorder_kv (rearrange_kv_cache, decoding.py:189-204; rearrange_mkv coreml.mm:251-277):
+// row j of window w continues row src[j]'s sequence.  The cache itself is not copied:
+// row j's ancestry (which beam slot holds each cached position) and history become
+// src[j]'s (k_append_tokens recorded each stepped position in its row's own slot).
+__global__ __launch_bounds__(256) void k_reorder_rows(DecState s, const int* __restrict__ src) {
+  __shared__ int oh[MG_MAXG][MG_MAXCTX];
+  __shared__ int oa[MG_MAXG][MG_MAXCTX];
+  const int w = blockIdx.x, tid = threadIdx.x, G = s.G;
+  const int len = s.len[w];
+  int* hist = s.hist + (int64_t)w * G * s.hctx;
+  int* anc = s.anc + (int64_t)w * G * s.ctx;
+  for (int i = tid; i < G * len; i += 256) {
+    const int b = i / len, p = i - b * len;
+    oh[b][p] = hist[b * s.hctx + p];
+    oa[b][p] = (p < s.ctx) ? anc[b * s.ctx + p] : 0;
+  }
+  __syncthreads();
+  for (int i = tid; i < G * len; i += 256) {
+    const int j = i / len, p = i - j * len;
+    const int sj = src[w * G + j] - w * G;
+    hist[j * s.hctx + p] = oh[sj][p];
+    if (p < s.ctx) anc[j * s.ctx + p] = oa[sj][p];
+  }
+}
+void launch_reorder_rows(const DecState& s, const int* src, int nwin, hipStream_t st) {
+  k_reorder_rows<<<nwin, 256, 0, st>>>(s, src);
 }
 
 // ------------------------------------------------------------ no_speech prob (decoding.py:716-720)

@@ -73,6 +73,7 @@ struct DecState {
   float* cand_val;   // [nw*G][KC]
   int* cand_idx;     // [nw*G][KC]
   float* lpart;      // [nw*G][LP_SLICES][LP_REC] per-slice token-selection partials
+  unsigned long long* seed;  // [1] sampling seed (device memory: not part of a captured graph)
   int nw, G, ctx, hctx, maxc;
 };
 
@@ -86,13 +87,15 @@ struct DecOpts {
   int sample_len;                    // max updates
   int n_ctx;                         // text context (448): stop when len > n_ctx
   float temperature;                 // > 0: Gumbel-max sampling (greedy decoder)
-  unsigned long long seed;
 };
 
 constexpr int LP_SLICES = 8;  // vocabulary slices per row: 7 text slices + [timestamp_begin, V)
 constexpr int LP_REC = 32;    // words per slice record
 void launch_logit_rows(float* logits, int ldl, const DecState& s, const DecOpts& o, int nwin, hipStream_t st);
 void launch_merge(const DecState& s, const DecOpts& o, int nwin, hipStream_t st);
+// per-step ABI (wh_step / wh_reorder_kv): append host-chosen tokens, reorder rows
+void launch_append_tokens(const DecState& s, const int* tok, int nwin, hipStream_t st);
+void launch_reorder_rows(const DecState& s, const int* src, int nwin, hipStream_t st);
 void launch_no_speech(const float* logits, int ldl, int rows, int V, int no_speech, float* out, hipStream_t st);
 void launch_broadcast_rows(const float* src, int ld_src, const int* src_rows, float* dst, int ld_dst, int G, int nwin,
                            int V, hipStream_t st);

@@ -111,8 +111,12 @@ struct wh_ctx {
   virtual int read_xa(int slot, float* out) = 0;
   virtual int read_ckv(int slot, int layer, float* k, float* v) = 0;
   virtual int decode_begin(int n_win, const wh_decode_opts* o, const int* init, const int* n_init, int max_init,
-                           const int* sot_index) = 0;
+                           const int* sot_index, const int* slots) = 0;
   virtual int decode_steps(int max_steps, int* n_done) = 0;
+  virtual int step_prefill(int n_win, int G, const int* init, const int* n_init, int max_init, const int* sot_index,
+                           float* lg) = 0;
+  virtual int step_tokens(const int* tok, const int* offsets, float* lg) = 0;
+  virtual int reorder_kv(const int* src) = 0;
   virtual int decode_read(int slot, int* tokens, float* slp, int* len, int* fin_n, int* fin_tok, int* fin_len,
                           float* fin_score, float* nsp) = 0;
   virtual int prefill_logits(int slot, const int* tokens, int n, float* logits, const int* ah, int na, float* aqk) = 0;
@@ -309,6 +313,7 @@ struct Ctx : public wh_ctx {
     addA((size_t)Wcap * Gcap * KC * 4); addA((size_t)Wcap * Gcap * KC * 4);
     addA((size_t)Wcap * Gcap * LP_SLICES * LP_REC * 4);
     addA(64);
+    addA(64);
     HIPCHK(hipMalloc(&abase, ab));
     HIPCHK(hipMemset(abase, 0, ab));
     aa.base = (char*)abase;
@@ -340,7 +345,8 @@ struct Ctx : public wh_ctx {
     S.fin_score = fa(Wcap * 16); S.fin_len = ia(Wcap * 16); S.fin_tok = ia((size_t)Wcap * 16 * HCTX);
     S.cand_val = fa((size_t)Wcap * Gcap * KC); S.cand_idx = ia((size_t)Wcap * Gcap * KC);
     S.lpart = fa((size_t)Wcap * Gcap * LP_SLICES * LP_REC);
-    if (!S.cand_idx) return fail(-3, "activation arena overflow");
+    S.seed = (unsigned long long*)aa.take(64);
+    if (!S.seed || !S.cand_idx) return fail(-3, "activation arena overflow");
     S.nw = Wcap; S.G = 1; S.ctx = CTX; S.hctx = HCTX; S.maxc = 16;
     HIPCHK(hipMalloc(&d_gmax, 64));
     d_gmax_f = (float*)(d_gmax + 4);
@@ -807,7 +813,8 @@ struct Ctx : public wh_ctx {
     O.blank[O.n_blank] = o->eot;  // SuppressBlank masks encode(" ") + [eot]
     O.n_blank += 1;
     O.suppress_blank = o->suppress_blank; O.timestamps = o->timestamps; O.max_initial = o->max_initial;
-    O.beam = o->beam; O.sample_len = o->sample_len; O.n_ctx = CTX; O.temperature = o->temperature; O.seed = o->seed;
+    O.beam = o->beam; O.sample_len = o->sample_len; O.n_ctx = CTX; O.temperature = o->temperature;
+    h_seed = o->seed;
     std::vector<unsigned> mask((V + 31) / 32, 0u);
     for (int i = 0; i < o->n_suppress; ++i) {
       const int t = o->suppress[i];
@@ -815,7 +822,11 @@ struct Ctx : public wh_ctx {
     }
     HIPCHK(hipMemcpyAsync(suppress, mask.data(), mask.size() * 4, hipMemcpyHostToDevice, st));
     O.suppress = o->n_suppress > 0 ? suppress : nullptr;
-    maxc = o->beam ? (int)std::lround(o->group * (o->patience > 0 ? o->patience : 1.0f)) : 0;
+    // max_candidates = round(beam_size * patience) (decoding.py:339): Python rounds half
+    // to even; the host passes its own value, else nearbyint (default mode: half to even)
+    maxc = !o->beam ? 0
+           : o->max_candidates > 0 ? o->max_candidates
+                                   : (int)std::nearbyint((double)o->group * (o->patience > 0 ? o->patience : 1.0));
     if (o->beam && (maxc < 1 || maxc > 16)) return fail(-11, "max_candidates out of range (1..16)");
     S.G = o->group;
     S.maxc = 16;
@@ -829,7 +840,7 @@ struct Ctx : public wh_ctx {
     for (int i = 0; i < nw; ++i) {
       wr0[i] = (int)rt.size();
       wnr[i] = nin[i];
-      wsl[i] = w0 + i;
+      wsl[i] = win_slots[w0 + i];
       for (int p = 0; p < nin[i]; ++p) {
         rt.push_back(toks[(size_t)i * HCTX + p]);
         rp.push_back(p);
@@ -857,13 +868,26 @@ struct Ctx : public wh_ctx {
     return 0;
   }
 
-  int decode_begin(int n_win, const wh_decode_opts* o, const int* init, const int* n_init, int max_init,
-                   const int* sot_index) override {
+  // prefill of the initial tokens of n_win windows (G rows each, sharing beam slot 0 of
+  // the self-KV), the decode state for step len = n_init[w], and the static step-row
+  // metadata.  Leaves the sot_index / last-row logits of window w in logits2 rows
+  // 2w / 2w+1 (and, when no_speech >= 0, its no-speech probability in nsp).
+  // Window w reads the audio features / cross-KV of slot slots[w] (identity when null):
+  // a temperature fallback decodes the windows that still need work straight from the
+  // slots that hold them, without re-running the encoder.
+  std::vector<int> h_len;      // host mirror of S.len for the per-step ABI
+  std::vector<int> win_slots;  // cross-KV slot of each decode window
+  unsigned long long h_seed = 0;
+  int begin_batch(int n_win, int G, const int* init, const int* n_init, int max_init, const int* sot_index,
+                  int no_speech, const int* slots = nullptr) {
     if (!finalized) return fail(-9, "weights not finalized");
     if (n_win < 1 || n_win > Wcap) return fail(-11, "n_win out of range");
-    TRY(set_opts(o));
-    const int G = o->group;
-    hipEventRecord(tm.a, st);
+    if (G < 1 || G > Gcap) return fail(-11, "group exceeds context max_group");
+    win_slots.resize(n_win);
+    for (int w = 0; w < n_win; ++w) {
+      win_slots[w] = slots ? slots[w] : w;
+      if (win_slots[w] < 0 || win_slots[w] >= Wcap) return fail(-11, "window slot out of range");
+    }
     // host-side initial state
     std::vector<int> hist((size_t)n_win * Gcap * HCTX, 0), anc((size_t)n_win * Gcap * CTX, 0), toks((size_t)n_win * HCTX, 0);
     std::vector<int> nin(n_win), lens(n_win), zeros(n_win, 0);
@@ -897,7 +921,7 @@ struct Ctx : public wh_ctx {
       w0 += nw;
     }
     // no_speech prob from the sot row of each window (decoding.py:716-720)
-    if (o->no_speech >= 0) launch_no_speech(logits2, 2 * V, n_win, V, o->no_speech, nsp, st);
+    if (no_speech >= 0) launch_no_speech(logits2, 2 * V, n_win, V, no_speech, nsp, st);
     // last-row logits replicated to the G rows of each window
     std::vector<int> src(n_win);
     for (int w = 0; w < n_win; ++w) src[w] = 2 * w + 1;
@@ -911,13 +935,12 @@ struct Ctx : public wh_ctx {
     HIPCHK(hipMemsetAsync(S.done, 0, n_win * 4, st));
     HIPCHK(hipMemsetAsync(S.fin_n, 0, n_win * 4, st));
     HIPCHK(hipMemsetAsync(S.sum_lp, 0, n_win * G * 4, st));
-    S.maxc = std::max(maxc, 1);
-    maxc_stride = S.maxc;
+    HIPCHK(hipMemcpyAsync(S.seed, &h_seed, 8, hipMemcpyHostToDevice, st));
     // static step-row metadata: row r = w*G + b
     std::vector<int> srw(n_win * G), srs(n_win * G), swr0(n_win), swnr(n_win, G), swsl(n_win);
     for (int w = 0; w < n_win; ++w) {
       swr0[w] = w * G;
-      swsl[w] = w;
+      swsl[w] = win_slots[w];
       for (int b = 0; b < G; ++b) { srw[w * G + b] = w; srs[w * G + b] = b; }
     }
     HIPCHK(hipMemcpyAsync(st_row_win, srw.data(), srw.size() * 4, hipMemcpyHostToDevice, st));
@@ -928,6 +951,22 @@ struct Ctx : public wh_ctx {
     // the self-KV cache uses [w][Gcap][..] slots; the anc table uses [w][G][..]
     cur_nwin = n_win;
     cur_G = G;
+    h_len = nin;
+    // the host vectors above must outlive the async copies
+    HIPCHK(hipStreamSynchronize(st));
+    return 0;
+  }
+
+  int decode_begin(int n_win, const wh_decode_opts* o, const int* init, const int* n_init, int max_init,
+                   const int* sot_index, const int* slots) override {
+    if (!finalized) return fail(-9, "weights not finalized");
+    if (n_win < 1 || n_win > Wcap) return fail(-11, "n_win out of range");
+    TRY(set_opts(o));
+    hipEventRecord(tm.a, st);
+    TRY(begin_batch(n_win, o->group, init, n_init, max_init, sot_index, o->no_speech, slots));
+    S.maxc = std::max(maxc, 1);
+    maxc_stride = S.maxc;
+    step_api = false;
     // first update on the prefill logits (decoding.py:713-733, i == 0)
     launch_logit_rows(logits, V, S, O, n_win, st);
     launch_merge(S, O, n_win, st);
@@ -949,6 +988,72 @@ struct Ctx : public wh_ctx {
     TRY(vocab(nullptr, R, logits));
     launch_logit_rows(logits, V, S, O, cur_nwin, st);
     launch_merge(S, O, cur_nwin, st);
+    return 0;
+  }
+
+  // ------------------------------------------------------------ per-step ABI
+  // The reference's native boundary hands every step's logits to the host and reorders
+  // the self-KV cache when the host asks (decoder256Predict coreml.mm:279-327,
+  // decoder1Predict :404-444, rearrange_mkv :251-277), so its Python DecodingTask keeps
+  // filters and beam search (decoding.py:707-737).  These entry points serve that
+  // caller: the same decoder step as the graph body, without the device token selection.
+  bool step_api = false;
+  int step_prefill(int n_win, int G, const int* init, const int* n_init, int max_init, const int* sot_index,
+                   float* lg) override {
+    hipEventRecord(tm.a, st);
+    TRY(begin_batch(n_win, G, init, n_init, max_init, sot_index, -1));
+    step_api = true;
+    if (lg) HIPCHK(hipMemcpyAsync(lg, logits2, (size_t)2 * n_win * V * 4, hipMemcpyDeviceToHost, st));
+    hipEventRecord(tm.b, st);
+    HIPCHK(hipStreamSynchronize(st));
+    HIPCHK(hipGetLastError());
+    float ms = 0;
+    hipEventElapsedTime(&ms, tm.a, tm.b);
+    stats[2] += ms;
+    return 0;
+  }
+
+  int step_tokens(const int* tok, const int* offsets, float* lg) override {
+    if (!step_api || cur_nwin < 1) return fail(-13, "no per-step batch (call wh_prefill first)");
+    const int R = cur_nwin * cur_G;
+    for (int r = 0; r < R; ++r)
+      if (tok[r] < 0 || tok[r] >= V) return fail(-13, "step token out of vocabulary");
+    for (int w = 0; w < cur_nwin; ++w) {
+      if (h_len[w] >= CTX) return fail(-13, "text context full (448 positions)");
+      if (offsets && offsets[w] != h_len[w])
+        return fail(-13, "text_offset " + std::to_string(offsets[w]) + " of window " + std::to_string(w) +
+                             " != cached length " + std::to_string(h_len[w]));
+    }
+    hipEventRecord(tm.a, st);
+    HIPCHK(hipMemcpyAsync(rows_in, tok, R * 4, hipMemcpyHostToDevice, st));
+    launch_append_tokens(S, rows_in, cur_nwin, st);
+    launch_embed<T>(E, Pdec, ns, nullptr, row_pos, S.hist, S.len, cur_G, HCTX, CTX - 1, x_d, R, st);
+    TRY(dec_layers(R, st_row_win, st_row_slot, row_pos, cur_G, cur_nwin, st_win_row0, st_win_nrows, st_win_slot,
+                   nullptr, nullptr, 0, true));
+    TRY(vocab(nullptr, R, logits));
+    if (lg) HIPCHK(hipMemcpyAsync(lg, logits, (size_t)R * V * 4, hipMemcpyDeviceToHost, st));
+    hipEventRecord(tm.b, st);
+    HIPCHK(hipStreamSynchronize(st));  // the host token buffer must outlive its copy
+    HIPCHK(hipGetLastError());
+    for (auto& l : h_len) ++l;
+    float ms = 0;
+    hipEventElapsedTime(&ms, tm.a, tm.b);
+    stats[3] += ms;
+    stats[4] += 1;
+    return 0;
+  }
+
+  int reorder_kv(const int* src) override {
+    if (!step_api || cur_nwin < 1) return fail(-13, "no per-step batch (call wh_prefill first)");
+    const int R = cur_nwin * cur_G;
+    for (int r = 0; r < R; ++r)
+      if (src[r] / cur_G != r / cur_G || src[r] < 0)
+        return fail(-13, "source row " + std::to_string(src[r]) + " of row " + std::to_string(r) +
+                             " is not a row of the same window");
+    HIPCHK(hipMemcpyAsync(src_rows, src, R * 4, hipMemcpyHostToDevice, st));
+    launch_reorder_rows(S, src_rows, cur_nwin, st);
+    HIPCHK(hipStreamSynchronize(st));
+    HIPCHK(hipGetLastError());
     return 0;
   }
 
@@ -994,6 +1099,7 @@ struct Ctx : public wh_ctx {
 
   int decode_steps(int max_steps, int* n_done) override {
     if (cur_nwin < 1) return fail(-13, "no decode in progress");
+    if (step_api) return fail(-13, "the batch was begun with wh_prefill (per-step mode): use wh_step");
     if (!eager()) TRY(ensure_graph());
     hipEventRecord(tm.a, st);
     int steps = 0, done = 0;
@@ -1478,7 +1584,12 @@ int wh_read_cross_kv(wh_ctx* ctx, int slot, int layer, float* k, float* v) { CTX
 int wh_decode_begin(wh_ctx* ctx, int n_win, const wh_decode_opts* o, const int* init, const int* n_init, int max_init,
                     const int* sot_index) {
   if (!o || !init || !n_init || !sot_index) return fail(-1, "null argument");
-  CTXCALL(ctx->decode_begin(n_win, o, init, n_init, max_init, sot_index));
+  CTXCALL(ctx->decode_begin(n_win, o, init, n_init, max_init, sot_index, nullptr));
+}
+int wh_decode_begin_slots(wh_ctx* ctx, int n_win, const int* slots, const wh_decode_opts* o, const int* init,
+                          const int* n_init, int max_init, const int* sot_index) {
+  if (!slots || !o || !init || !n_init || !sot_index) return fail(-1, "null argument");
+  CTXCALL(ctx->decode_begin(n_win, o, init, n_init, max_init, sot_index, slots));
 }
 int wh_decode_steps(wh_ctx* ctx, int max_steps, int* n_done) { CTXCALL(ctx->decode_steps(max_steps, n_done)); }
 int wh_decode_read(wh_ctx* ctx, int slot, int* tokens, float* slp, int* len, int* fin_n, int* fin_tok, int* fin_len,
@@ -1486,6 +1597,19 @@ int wh_decode_read(wh_ctx* ctx, int slot, int* tokens, float* slp, int* len, int
   CTXCALL(ctx->decode_read(slot, tokens, slp, len, fin_n, fin_tok, fin_len, fin_score, nsp));
 }
 int wh_decode_maxc(wh_ctx* ctx) { return ctx ? ctx->maxc_stride : -1; }
+int wh_prefill(wh_ctx* ctx, int n_win, int group, const int* tokens, const int* n_tokens, int max_tokens,
+               const int* sot_index, float* logits) {
+  if (!tokens || !n_tokens || !sot_index) return fail(-1, "null argument");
+  CTXCALL(ctx->step_prefill(n_win, group, tokens, n_tokens, max_tokens, sot_index, logits));
+}
+int wh_step(wh_ctx* ctx, const int* tokens, const int* text_offsets, float* logits) {
+  if (!tokens) return fail(-1, "null argument");
+  CTXCALL(ctx->step_tokens(tokens, text_offsets, logits));
+}
+int wh_reorder_kv(wh_ctx* ctx, const int* source_rows) {
+  if (!source_rows) return fail(-1, "null argument");
+  CTXCALL(ctx->reorder_kv(source_rows));
+}
 int wh_prefill_logits(wh_ctx* ctx, int slot, const int* tokens, int n, float* logits, const int* ah, int na, float* aqk) {
   CTXCALL(ctx->prefill_logits(slot, tokens, n, logits, ah, na, aqk));
 }

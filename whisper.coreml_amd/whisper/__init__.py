@@ -6,11 +6,11 @@ Mirrors the public surface of the reference package (whisper/__init__.py:102-179
 ``load_audio``.  ``load_model(..., use_coreml=...)`` is accepted for call-site
 compatibility and ignored: the compute backend is always libwhisper_hip.so.
 
-There is no network: a model name resolves to ``<download_root>/<name>.pt`` when
-that checkpoint exists, otherwise (``synthetic=True``, the default when no file
-is found) to a seeded synthetic checkpoint with the official dimensions
-(whisper/synthetic.py).  A path loads ``{"dims", "model_state_dict"}`` with
-``torch.load(weights_only=True)``.
+There is no network: a model name resolves to ``<download_root>/<name>.pt``; a
+missing checkpoint raises, as the reference's loader does without a download.
+Seeded synthetic weights with the official dimensions (whisper/synthetic.py) are
+opt-in: ``synthetic=True`` or ``WHISPER_HIP_SYNTHETIC=1``.  A path loads
+``{"dims", "model_state_dict"}`` with ``torch.load(weights_only=True)``.
 """
 
 import os
@@ -74,10 +74,13 @@ def load_model(name: str, device: Optional[Union[str, int]] = None, download_roo
     align = None
     if name in MODEL_DIMS:
         p = os.path.join(download_root, f"{name}.pt")
+        if synthetic is None:
+            synthetic = os.environ.get("WHISPER_HIP_SYNTHETIC", "0") == "1"
         if os.path.isfile(p) and not synthetic:
             ckpt = p
-        elif synthetic is False:
-            raise RuntimeError(f"Model {name} not found in {download_root} (no network to download it)")
+        elif not synthetic:
+            raise RuntimeError(f"Model {name} not found in {download_root} (no network to download it; "
+                               f"synthetic=True loads seeded random weights instead)")
         align = _ALIGNMENT_HEADS.get(name)
     elif os.path.isfile(name):
         ckpt = name
@@ -89,7 +92,7 @@ def load_model(name: str, device: Optional[Union[str, int]] = None, download_roo
         dims = ModelDimensions(**checkpoint["dims"])
         state = checkpoint["model_state_dict"]
     else:
-        warnings.warn(f"no checkpoint for {name!r}: using seeded synthetic weights (seed={seed})")
+        warnings.warn(f"{name!r}: seeded synthetic weights (seed={seed}), not a trained checkpoint")
         dims = ModelDimensions(**MODEL_DIMS[name])
         state = synthetic_state_dict(MODEL_DIMS[name], seed)
     model = Whisper(dims, name, device=dev, dtype=dtype, max_windows=max_windows, max_group=max_group)

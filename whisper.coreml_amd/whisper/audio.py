@@ -93,7 +93,7 @@ def _mel_to_hz(m):
 def mel_filters(device=None, n_mels: int = 80) -> np.ndarray:
     """Slaney-normalised mel filterbank [n_mels][201] — the values the reference
     loads from assets/mel_filters.npz (audio.py:91-107, librosa.filters.mel with
-    sr=16000, n_fft=400), re-derived here and pinned by tests/test_audio.py."""
+    sr=16000, n_fft=400), re-derived here and pinned to the reference values by tests/test_audio_mel.py."""
     assert n_mels in {80, 128}, f"Unsupported n_mels: {n_mels}"
     fft_freqs = np.linspace(0, SAMPLE_RATE / 2, 1 + N_FFT // 2)
     mel_f = _mel_to_hz(np.linspace(_hz_to_mel(0.0), _hz_to_mel(SAMPLE_RATE / 2), n_mels + 2))

@@ -37,7 +37,7 @@ class WhDecodeOpts(ctypes.Structure):
                 ("sample_len", c_int), ("suppress_blank", c_int), ("timestamps", c_int), ("max_initial", c_int),
                 ("eot", c_int), ("no_speech", c_int), ("no_timestamps", c_int), ("timestamp_begin", c_int),
                 ("blank", c_int * 4), ("n_blank", c_int), ("suppress", POINTER(c_int)), ("n_suppress", c_int),
-                ("seed", c_uint64)]
+                ("seed", c_uint64), ("max_candidates", c_int)]
 
 
 _lib = None
@@ -62,10 +62,15 @@ _EXPORTS = {
     "wh_read_audio_features": (c_int, [c_void_p, c_int, c_void_p]),
     "wh_read_cross_kv": (c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p]),
     "wh_decode_begin": (c_int, [c_void_p, c_int, POINTER(WhDecodeOpts), c_void_p, c_void_p, c_int, c_void_p]),
+    "wh_decode_begin_slots": (c_int, [c_void_p, c_int, c_void_p, POINTER(WhDecodeOpts), c_void_p, c_void_p, c_int,
+                                      c_void_p]),
     "wh_decode_steps": (c_int, [c_void_p, c_int, POINTER(c_int)]),
     "wh_decode_read": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                c_void_p, c_void_p]),
     "wh_decode_maxc": (c_int, [c_void_p]),
+    "wh_prefill": (c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p]),
+    "wh_step": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p]),
+    "wh_reorder_kv": (c_int, [c_void_p, c_void_p]),
     "wh_prefill_logits": (c_int, [c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p]),
     "wh_align": (c_int, [c_void_p, c_int, c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_int, c_void_p, c_void_p,
                          POINTER(c_int)]),
@@ -252,7 +257,9 @@ class HipContext:
         return k, v
 
     # -- decoding
-    def decode_begin(self, opts: WhDecodeOpts, init_tokens: Sequence[Sequence[int]], sot_index: Sequence[int]):
+    def decode_begin(self, opts: WhDecodeOpts, init_tokens: Sequence[Sequence[int]], sot_index: Sequence[int],
+                     slots: Optional[Sequence[int]] = None):
+        """Decode window w = init_tokens[w] over encoder slot slots[w] (default w)."""
         n = len(init_tokens)
         mx = max(len(t) for t in init_tokens)
         arr = np.zeros((n, mx), dtype=np.int32)
@@ -260,8 +267,14 @@ class HipContext:
             arr[i, :len(t)] = t
         nin = np.asarray([len(t) for t in init_tokens], dtype=np.int32)
         si = np.asarray(sot_index, dtype=np.int32)
-        self._check(self.lib.wh_decode_begin(self.h, n, ctypes.byref(opts), _ptr(arr), _ptr(nin), mx, _ptr(si)),
-                    "wh_decode_begin")
+        if slots is None:
+            self._check(self.lib.wh_decode_begin(self.h, n, ctypes.byref(opts), _ptr(arr), _ptr(nin), mx, _ptr(si)),
+                        "wh_decode_begin")
+        else:
+            sl = np.ascontiguousarray(slots, dtype=np.int32)
+            assert len(sl) == n
+            self._check(self.lib.wh_decode_begin_slots(self.h, n, _ptr(sl), ctypes.byref(opts), _ptr(arr), _ptr(nin),
+                                                       mx, _ptr(si)), "wh_decode_begin_slots")
 
     def decode_steps(self, max_steps: int) -> int:
         nd = c_int()
@@ -284,6 +297,37 @@ class HipContext:
         n = int(fn[0])
         return dict(tokens=toks, sum_logprobs=slp, length=int(ln[0]), fin_tokens=ftok[:n], fin_len=flen[:n],
                     fin_score=fsc[:n], no_speech_prob=float(nsp[0]))
+
+    # -- per-step boundary (decoder256Predict / decoder1Predict / rearrange_mkv roles)
+    def prefill(self, init_tokens: Sequence[Sequence[int]], group: int, sot_index: Sequence[int],
+                logits: bool = True):
+        """wh_prefill: first pass of each window's initial tokens (windows = slots
+        0..n-1); returns [n][2][V] logits at (sot_index, last) or None."""
+        n = len(init_tokens)
+        mx = max(len(t) for t in init_tokens)
+        arr = np.zeros((n, mx), dtype=np.int32)
+        for i, t in enumerate(init_tokens):
+            arr[i, :len(t)] = t
+        nin = np.asarray([len(t) for t in init_tokens], dtype=np.int32)
+        si = np.asarray(sot_index, dtype=np.int32)
+        out = np.empty((n, 2, self.dims["n_vocab"]), dtype=np.float32) if logits else None
+        self._check(self.lib.wh_prefill(self.h, n, int(group), _ptr(arr), _ptr(nin), mx, _ptr(si),
+                                        _ptr(out) if out is not None else None), "wh_prefill")
+        return out
+
+    def step(self, tokens: Sequence[int], text_offsets: Optional[Sequence[int]] = None, logits: bool = True):
+        """wh_step: rows append ``tokens`` and run one decoder step; [rows][V] logits."""
+        t = np.ascontiguousarray(tokens, dtype=np.int32)
+        off = None if text_offsets is None else np.ascontiguousarray(text_offsets, dtype=np.int32)
+        out = np.empty((len(t), self.dims["n_vocab"]), dtype=np.float32) if logits else None
+        self._check(self.lib.wh_step(self.h, _ptr(t), _ptr(off) if off is not None else None,
+                                     _ptr(out) if out is not None else None), "wh_step")
+        return out
+
+    def reorder_kv(self, source_rows: Sequence[int]):
+        """wh_reorder_kv: row r continues row source_rows[r] (same window)."""
+        s = np.ascontiguousarray(source_rows, dtype=np.int32)
+        self._check(self.lib.wh_reorder_kv(self.h, _ptr(s)), "wh_reorder_kv")
 
     def prefill_logits(self, slot: int, tokens: Sequence[int], align_heads: Sequence[int] = ()):
         t = np.asarray(tokens, dtype=np.int32)

@@ -135,6 +135,8 @@ class DecodingTask:
         w.group = self.n_group
         w.beam = 1 if o.beam_size is not None else 0
         w.patience = float(o.patience or 1.0)
+        # max_candidates = round(beam_size * patience) with Python's rounding (decoding.py:339)
+        w.max_candidates = round(self.n_group * (o.patience or 1.0)) if o.beam_size is not None else 0
         w.temperature = float(o.temperature) if o.beam_size is None else 0.0
         w.sample_len = self.sample_len
         w.suppress_blank = int(o.suppress_blank)
@@ -185,14 +187,14 @@ class DecodingTask:
 
 
 def run_windows(model: "Whisper", options: DecodingOptions, prompts: Sequence[Optional[List[int]]],
-                audio_features: bool = False) -> List[DecodingResult]:
-    """Decode windows already encoded into slots 0..len(prompts)-1 of the model's
-    context, all with ``options`` except the per-window prompt."""
+                audio_features: bool = False, slots: Optional[Sequence[int]] = None) -> List[DecodingResult]:
+    """Decode windows already encoded into the model's context: window i uses encoder
+    slot ``slots[i]`` (default i), all with ``options`` except the per-window prompt."""
     tasks = [DecodingTask(model, replace(options, prompt=p)) for p in prompts]
     t0 = tasks[0]
     opts = t0.wh_opts()
     ctx = model.ctx
-    ctx.decode_begin(opts, [t.initial_tokens for t in tasks], [t.sot_index for t in tasks])
+    ctx.decode_begin(opts, [t.initial_tokens for t in tasks], [t.sot_index for t in tasks], slots=slots)
     # every window stops on the device (completion, n_ctx or sample_len updates);
     # decode_steps returns once all of them are done
     ctx.decode_steps(t0.sample_len)
@@ -203,7 +205,8 @@ def run_windows(model: "Whisper", options: DecodingOptions, prompts: Sequence[Op
         toks, _, avg = t.finalize(raw)
         text = t.tokenizer.decode(toks).strip()
         out.append(DecodingResult(
-            audio_features=ctx.audio_features(i) if audio_features else None, language=lang, tokens=toks,
+            audio_features=ctx.audio_features(slots[i] if slots is not None else i) if audio_features else None,
+            language=lang, tokens=toks,
             text=text, avg_logprob=avg, no_speech_prob=raw["no_speech_prob"], temperature=options.temperature,
             compression_ratio=compression_ratio(text) if text else _token_compression_ratio(toks)))
     return out

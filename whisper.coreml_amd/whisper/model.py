@@ -76,15 +76,7 @@ class Whisper:
     def close(self):
         self.ctx.close()
 
-    _last_windows = ([], [])
-
-    def _reencode(self, indices):
-        """Re-encode a subset of the last encoded windows into slots 0..k-1
-        (temperature fallback keeps only the windows that still need work)."""
-        seeks, segs = self._last_windows
-        sub = ([seeks[i] for i in indices], [segs[i] for i in indices])
-        self.ctx.encode(*sub)
-        self._last_windows = sub
+    _last_windows = ([], [])  # (seeks, sizes) of the windows in the encoder slots
 
     from .decoding import decode as decode  # noqa: E402
     from .decoding import detect_language as detect_language  # noqa: E402

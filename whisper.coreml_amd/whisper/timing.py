@@ -5,7 +5,8 @@ heads' cross-QK, the text-token probabilities, softmax / z-norm / median filter 
 head mean and the DTW with its backtrace — runs in libwhisper_hip (``wh_align``,
 csrc/wh_align.hip).  What stays here is the reference's host logic on the returned
 path: word splitting, jump times, punctuation merging and the segment-level
-refinements of ``add_word_timestamps`` (timing.py:234-376), restated line by line.
+refinements of ``add_word_timestamps`` (timing.py:234-376), pinned to the reference's
+own outputs by tests/golden/micro_words.json.
 """
 
 import itertools
@@ -95,34 +96,33 @@ def _words_from_path(tokenizer: Tokenizer, text_tokens: List[int], probs: np.nda
 
 
 def merge_punctuations(alignment: List[WordTiming], prepended: str, appended: str):
-    """timing.py:234-265."""
-    i = len(alignment) - 2
-    j = len(alignment) - 1
-    while i >= 0:
-        previous = alignment[i]
-        following = alignment[j]
-        if previous.word.startswith(" ") and previous.word.strip() in prepended:
-            following.word = previous.word + following.word
-            following.tokens = previous.tokens + following.tokens
-            previous.word = ""
-            previous.tokens = []
+    """timing.py:234-265, in place: opening punctuation (a word " X" with X in
+    `prepended`) moves onto the next word that is not itself such punctuation (the last
+    word always takes what is pending); closing punctuation (a word in `appended`)
+    moves onto the nearest kept word before it unless that word ends in a space.
+    Moved words stay in the list with empty text and tokens."""
+    pending: List[WordTiming] = []
+    last = len(alignment) - 1
+    for k, w in enumerate(alignment):
+        if k < last and w.word.startswith(" ") and w.word.strip() in prepended:
+            pending.append(w)
+            continue
+        if pending:
+            w.word = "".join(p.word for p in pending) + w.word
+            w.tokens = [t for p in pending for t in p.tokens] + w.tokens
+            for p in pending:
+                p.word, p.tokens = "", []
+            pending = []
+    if not alignment:
+        return
+    host = alignment[0]
+    for w in alignment[1:]:
+        if not host.word.endswith(" ") and w.word in appended:
+            host.word += w.word
+            host.tokens = host.tokens + w.tokens
+            w.word, w.tokens = "", []
         else:
-            j = i
-        i -= 1
-
-    i = 0
-    j = 1
-    while j < len(alignment):
-        previous = alignment[i]
-        following = alignment[j]
-        if not previous.word.endswith(" ") and following.word in appended:
-            previous.word = previous.word + following.word
-            previous.tokens = previous.tokens + following.tokens
-            following.word = ""
-            following.tokens = []
-        else:
-            i = j
-        j += 1
+            host = w
 
 
 def add_word_timestamps(*, segments: List[dict], model: "Whisper", tokenizer: Tokenizer, num_frames: int,
@@ -142,70 +142,76 @@ def _text_tokens_per_segment(segments: List[dict], tokenizer: Tokenizer) -> List
     return [[token for token in segment["tokens"] if token < tokenizer.eot] for segment in segments]
 
 
+def _duration_limits(alignment: List[WordTiming]):
+    """(median, max) word duration of timing.py:292-296: the median over non-zero
+    durations, capped at 0.7 s; the max is twice that."""
+    d = np.array([w.end - w.start for w in alignment])
+    d = d[d.nonzero()]
+    med = min(0.7, float(np.median(d) if len(d) > 0 else 0.0))
+    return med, 2 * med, len(d) > 0
+
+
+def _clip_at_sentence_marks(alignment: List[WordTiming], max_duration: float):
+    """timing.py:301-312: a too-long word that is a sentence end mark keeps its start;
+    a too-long word right after one keeps its end."""
+    marks = ".。!！?？"
+    for prev, w in zip(alignment, alignment[1:]):
+        if w.end - w.start <= max_duration:
+            continue
+        if w.word in marks:
+            w.end = w.start + max_duration
+        elif prev.word in marks:
+            w.start = w.end - max_duration
+
+
+def _fit_segment_words(segment: dict, words: List[dict], last_speech: float, med: float, max_d: float) -> float:
+    """timing.py:343-374 for one segment: shorten an overlong first word after a pause,
+    then reconcile the segment's bounds with its first / last word.  Returns the new
+    last-speech time."""
+    first, last = words[0], words[-1]
+    second = words[1] if len(words) > 1 else None
+    too_long = first["end"] - first["start"] > max_d or (
+        second is not None and second["end"] - first["start"] > 2 * max_d)
+    if first["end"] - last_speech > 4 * med and too_long:
+        if second is not None and second["end"] - second["start"] > max_d:
+            cut = max(second["end"] / 2, second["end"] - max_d)
+            first["end"] = second["start"] = cut
+        first["start"] = max(0, first["end"] - max_d)
+    if segment["start"] < first["end"] and segment["start"] - 0.5 > first["start"]:
+        first["start"] = max(0, min(first["end"] - med, segment["start"]))
+    else:
+        segment["start"] = first["start"]
+    if segment["end"] > last["start"] and segment["end"] + 0.5 < last["end"]:
+        last["end"] = max(last["start"] + med, segment["end"])
+    else:
+        segment["end"] = last["end"]
+    return segment["end"]
+
+
 def apply_alignment(segments: List[dict], alignment: List[WordTiming], tokenizer: Tokenizer,
                     prepend_punctuations: str, append_punctuations: str, last_speech_timestamp: float):
     """The host half of add_word_timestamps (timing.py:292-376) on an alignment from
-    find_alignment (mutated: pass a copy to keep it)."""
+    find_alignment (mutated: pass a copy to keep it).  Words are dealt to segments in
+    order until each segment's text-token count is covered; emptied (merged)
+    punctuation entries consume their tokens without producing a word."""
     if len(segments) == 0:
         return
-    text_tokens_per_segment = _text_tokens_per_segment(segments, tokenizer)
-    word_durations = np.array([t.end - t.start for t in alignment])
-    word_durations = word_durations[word_durations.nonzero()]
-    median_duration = np.median(word_durations) if len(word_durations) > 0 else 0.0
-    median_duration = min(0.7, float(median_duration))
-    max_duration = median_duration * 2
-
-    # truncate long words at sentence boundaries (timing.py:301-312)
-    if len(word_durations) > 0:
-        sentence_end_marks = ".。!！?？"
-        for i in range(1, len(alignment)):
-            if alignment[i].end - alignment[i].start > max_duration:
-                if alignment[i].word in sentence_end_marks:
-                    alignment[i].end = alignment[i].start + max_duration
-                elif alignment[i - 1].word in sentence_end_marks:
-                    alignment[i].start = alignment[i].end - max_duration
-
+    med, max_d, any_duration = _duration_limits(alignment)
+    if any_duration:
+        _clip_at_sentence_marks(alignment, max_d)
     merge_punctuations(alignment, prepend_punctuations, append_punctuations)
-
-    time_offset = segments[0]["seek"] * HOP_LENGTH / SAMPLE_RATE
-    word_index = 0
-
-    for segment, text_tokens in zip(segments, text_tokens_per_segment):
-        saved_tokens = 0
-        words = []
-
-        while word_index < len(alignment) and saved_tokens < len(text_tokens):
-            timing = alignment[word_index]
-
+    t0 = segments[0]["seek"] * HOP_LENGTH / SAMPLE_RATE
+    source = iter(alignment)
+    for segment, need in zip(segments, (len(t) for t in _text_tokens_per_segment(segments, tokenizer))):
+        words, covered = [], 0
+        while covered < need:
+            timing = next(source, None)
+            if timing is None:
+                break
+            covered += len(timing.tokens)
             if timing.word:
-                words.append(dict(word=timing.word, start=round(time_offset + timing.start, 2),
-                                  end=round(time_offset + timing.end, 2), probability=timing.probability))
-
-            saved_tokens += len(timing.tokens)
-            word_index += 1
-
-        # truncate long words at segment boundaries (timing.py:343-360)
-        if len(words) > 0:
-            if words[0]["end"] - last_speech_timestamp > median_duration * 4 and (
-                    words[0]["end"] - words[0]["start"] > max_duration
-                    or (len(words) > 1 and words[1]["end"] - words[0]["start"] > max_duration * 2)):
-                if len(words) > 1 and words[1]["end"] - words[1]["start"] > max_duration:
-                    boundary = max(words[1]["end"] / 2, words[1]["end"] - max_duration)
-                    words[0]["end"] = words[1]["start"] = boundary
-                words[0]["start"] = max(0, words[0]["end"] - max_duration)
-
-            # prefer the segment-level start timestamp if the first word is too long
-            if segment["start"] < words[0]["end"] and segment["start"] - 0.5 > words[0]["start"]:
-                words[0]["start"] = max(0, min(words[0]["end"] - median_duration, segment["start"]))
-            else:
-                segment["start"] = words[0]["start"]
-
-            # prefer the segment-level end timestamp if the last word is too long
-            if segment["end"] > words[-1]["start"] and segment["end"] + 0.5 < words[-1]["end"]:
-                words[-1]["end"] = max(words[-1]["start"] + median_duration, segment["end"])
-            else:
-                segment["end"] = words[-1]["end"]
-
-            last_speech_timestamp = segment["end"]
-
+                words.append(dict(word=timing.word, start=round(t0 + timing.start, 2), end=round(t0 + timing.end, 2),
+                                  probability=timing.probability))
+        if words:
+            last_speech_timestamp = _fit_segment_words(segment, words, last_speech_timestamp, med, max_d)
         segment["words"] = words

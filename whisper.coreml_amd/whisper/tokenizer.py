@@ -4,10 +4,10 @@ The hot path needs only ids: special tokens (laid out after the base BPE ranks
 exactly as ``get_encoding`` does, tokenizer.py:331-363), the SuppressTokens
 ``-1`` set (``non_speech_tokens``, tokenizer.py:253-284) and ``encode(" ")``.
 Those facts ship as data in assets/specials.json (exported from the reference
-tokenizer by oracle/gen_golden.py).  Text needs the BPE rank file
-(``multilingual.tiktoken`` / ``gpt2.tiktoken``); point WHISPER_TIKTOKEN_DIR at a
-directory holding it (the tests use tests/golden/) to enable ``decode`` and
-``encode``; without it ``decode`` returns "" and ``encode`` raises.  ``encode`` is
+tokenizer by oracle/gen_golden.py).  Text needs the BPE rank files
+(``multilingual.tiktoken`` / ``gpt2.tiktoken``, data the reference ships in
+whisper/assets): they ship in assets/ too, WHISPER_TIKTOKEN_DIR overrides the
+directory, and ``decode`` / ``encode`` raise when a file is missing.  ``encode`` is
 tiktoken's byte-level BPE restated (tiktoken is a Rust dependency of the reference,
 unpinned in requirements.txt; tokenizer.py:331-363 builds the Encoding): the text is
 split by the encoding's regex, each piece's UTF-8 bytes are merged pairwise, lowest
@@ -55,9 +55,9 @@ def _ranks(name: str) -> Optional[Dict[int, bytes]]:
 
 @lru_cache(maxsize=None)
 def _rank_file(name: str) -> Optional[Dict[int, bytes]]:
-    d = os.environ.get("WHISPER_TIKTOKEN_DIR")
-    if not d:
-        return None
+    """BPE ranks of `name` from WHISPER_TIKTOKEN_DIR if set, else the package assets
+    (the reference ships the same two files in whisper/assets, tokenizer.py:332-336)."""
+    d = os.environ.get("WHISPER_TIKTOKEN_DIR") or _ASSETS
     p = os.path.join(d, f"{name}.tiktoken")
     if not os.path.exists(p):
         return None
@@ -202,8 +202,8 @@ class Tokenizer:
         """tokenizer.py:148-149 (``encoding.encode(text)``: plain text, no specials)."""
         enc = _encoder(self.encoding_name)
         if enc is None:
-            raise RuntimeError("encode needs the BPE rank file: set WHISPER_TIKTOKEN_DIR to a directory holding "
-                               f"{self.encoding_name}.tiktoken")
+            raise RuntimeError(f"encode needs the BPE rank file {self.encoding_name}.tiktoken "
+                               "(whisper/assets or WHISPER_TIKTOKEN_DIR)")
         rank, pat = enc
         out: List[int] = []
         for piece in pat.findall(text):
@@ -213,7 +213,8 @@ class Tokenizer:
     def decode(self, token_ids: List[int]) -> str:
         ranks = _ranks(self.encoding_name)
         if ranks is None:
-            return ""
+            raise RuntimeError(f"decode needs the BPE rank file {self.encoding_name}.tiktoken "
+                               "(whisper/assets or WHISPER_TIKTOKEN_DIR)")
         b = b"".join(ranks[t] for t in token_ids if t < self.timestamp_begin and t in ranks)
         return b.decode("utf-8", errors="replace")
 
@@ -231,52 +232,54 @@ class Tokenizer:
 
     # word splitting for word-level timestamps (tokenizer.py:277-327)
     def split_to_word_tokens(self, tokens: List[int]):
+        """(words, word_tokens).  Tokens are first grouped into UTF-8-complete pieces;
+        for space-delimited languages a piece then starts a new word if it is a special
+        token, begins with a space, is punctuation, or is the first piece; otherwise it
+        extends the previous word."""
         if _ranks(self.encoding_name) is None:
-            raise RuntimeError("word timestamps need the BPE rank file: set WHISPER_TIKTOKEN_DIR "
-                               f"to a directory holding {self.encoding_name}.tiktoken")
+            raise RuntimeError("word timestamps need the BPE rank file "
+                               f"{self.encoding_name}.tiktoken (whisper/assets or WHISPER_TIKTOKEN_DIR)")
+        pieces = self._utf8_pieces(tokens)
         if self.language in {"zh", "ja", "th", "lo", "my", "yue"}:
-            return self.split_tokens_on_unicode(tokens)
-        return self.split_tokens_on_spaces(tokens)
+            return [p for p, _ in pieces], [ids for _, ids in pieces]
+        words: List[str] = []
+        ids: List[List[int]] = []
+        for text, group in pieces:
+            if not words or group[0] >= self.eot or text.startswith(" ") or text.strip() in string.punctuation:
+                words.append(text)
+                ids.append(list(group))
+            else:
+                words[-1] += text
+                ids[-1].extend(group)
+        return words, ids
 
     def split_tokens_on_unicode(self, tokens: List[int]):
-        decoded_full = self.decode_with_timestamps(tokens)
-        replacement_char = "\ufffd"
-
-        words = []
-        word_tokens = []
-        current_tokens = []
-        unicode_offset = 0
-
-        for token in tokens:
-            current_tokens.append(token)
-            decoded = self.decode_with_timestamps(current_tokens)
-
-            if (replacement_char not in decoded
-                    or decoded_full[unicode_offset + decoded.index(replacement_char)] == replacement_char):
-                words.append(decoded)
-                word_tokens.append(current_tokens)
-                current_tokens = []
-                unicode_offset += len(decoded)
-
-        return words, word_tokens
+        pieces = self._utf8_pieces(tokens)
+        return [p for p, _ in pieces], [ids for _, ids in pieces]
 
     def split_tokens_on_spaces(self, tokens: List[int]):
-        subwords, subword_tokens_list = self.split_tokens_on_unicode(tokens)
-        words = []
-        word_tokens = []
+        return self.split_to_word_tokens(tokens)
 
-        for subword, subword_tokens in zip(subwords, subword_tokens_list):
-            special = subword_tokens[0] >= self.eot
-            with_space = subword.startswith(" ")
-            punctuation = subword.strip() in string.punctuation
-            if special or with_space or punctuation or len(words) == 0:
-                words.append(subword)
-                word_tokens.append(subword_tokens)
-            else:
-                words[-1] = words[-1] + subword
-                word_tokens[-1].extend(subword_tokens)
+    def _utf8_pieces(self, tokens: List[int]) -> List[Tuple[str, List[int]]]:
+        """Consecutive tokens whose bytes decode together (tokenizer.py:286-311): a
+        piece ends at the first token after which its text has no U+FFFD, or after
+        which its first U+FFFD is also present at that place of the whole text (bytes
+        that no following token completes)."""
+        raw = [self._token_bytes(t) for t in tokens]
+        whole = b"".join(raw).decode("utf-8", errors="replace")
+        out: List[Tuple[str, List[int]]] = []
+        begin, chars = 0, 0
+        for stop in range(1, len(tokens) + 1):
+            text = b"".join(raw[begin:stop]).decode("utf-8", errors="replace")
+            bad = text.find("\ufffd")
+            if bad < 0 or whole[chars + bad] == "\ufffd":
+                out.append((text, list(tokens[begin:stop])))
+                begin, chars = stop, chars + len(text)
+        return out
 
-        return words, word_tokens
+    def _token_bytes(self, t: int) -> bytes:
+        ranks = _ranks(self.encoding_name) or {}
+        return ranks[t] if t in ranks else self._special_bytes().get(t, b"")
 
 
 @lru_cache(maxsize=None)

@@ -41,7 +41,9 @@ if TYPE_CHECKING:
 
 def _decode_with_fallback(model, base_opts: DecodingOptions, temperatures, prompts: List, thresholds
                           ) -> List[DecodingResult]:
-    """transcribe.py:188-228 for a batch of windows (slots 0..n-1 already encoded)."""
+    """transcribe.py:188-228 for a batch of windows (slots 0..n-1 already encoded).
+    A retry at the next temperature decodes only the windows that still need work,
+    from the encoder slots that already hold their audio features (no re-encode)."""
     cr_thr, lp_thr, ns_thr = thresholds
     n = len(prompts)
     results: List[Optional[DecodingResult]] = [None] * n
@@ -55,10 +57,8 @@ def _decode_with_fallback(model, base_opts: DecodingOptions, temperatures, promp
         opts = replace(base_opts, temperature=t, **kw)
         if t > 0 and opts.best_of is None:
             opts = replace(opts, best_of=None)
-        if pending != list(range(n)):
-            # re-encode only the windows that still need work: keep slot order stable
-            model._reencode(pending)
-        res = run_windows(model, opts, [prompts[i] for i in pending])
+        res = run_windows(model, opts, [prompts[i] for i in pending],
+                          slots=None if pending == list(range(n)) else pending)
         nxt = []
         for i, r in zip(pending, res):
             results[i] = r
@@ -363,9 +363,6 @@ def _run_sequential(model, clips, initial_prompt_tokens, condition_on_previous_t
         if skipped:
             continue
         if st["word_timestamps"]:
-            if model._last_windows != ([previous_seek], [segment_size]):
-                ctx.encode([previous_seek], [segment_size])
-                model._last_windows = ([previous_seek], [segment_size])
             alignment = _window_alignment(model, st, segs, segment_size, 0) if segs else []
             seek = _words_and_seek(st, segs, alignment, seek, previous_seek, segment_size, single_end,
                                    last_speech_timestamp)
@@ -458,10 +455,6 @@ def _run_batched(model, clips, initial_prompt_tokens, st):
             ctx.encode([s for _, s, _ in chunk], [z for _, _, z in chunk])
             model._last_windows = ([s for _, s, _ in chunk], [z for _, _, z in chunk])
             results = _decode_with_fallback(model, st["base"], st["temperatures"], prompts, st["thresholds"])
-            wins = ([s for _, s, _ in chunk], [z for _, _, z in chunk])
-            if st["word_timestamps"] and model._last_windows != wins:
-                ctx.encode(*wins)  # fallback re-encoded a subset: restore slot order
-                model._last_windows = wins
             applied = [_apply_result(model, r, seek, segment_size, st) for (ci, seek, segment_size), r in
                        zip(chunk, results)]
             if st["word_timestamps"]:
