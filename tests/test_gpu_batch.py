@@ -12,7 +12,8 @@ Bars (DESIGN.md §2 states them):
     wh_prefill / wh_step / wh_reorder_kv, tokens and beam reorders supplied, not
     selected): at every one of the 224 steps and every row,
         max |logit - ref| over the reference top-32  <=  TAU[dtype] * (top-32 range)
-    with TAU = 2e-4 (fp32) and 3e-2 (fp16), at 1 and 20 windows (5 / 100 rows);
+    with TAU = 2e-5 (fp32) and 1e-2 (fp16), at 1 and 20 windows (5 / 100 rows)
+    (measured worst cases, profiles/r02/gpu_tests.log: 7.6e-6 and 3.3e-3);
   * the reference's host loop (decoding.py:707-737, restated by the oracle) driving
     the per-step ABI through whisper.inference.HipInference: fp32 tokens exact.
 """
@@ -25,7 +26,7 @@ from conftest import GOLDEN, full_model, golden_window
 
 pytestmark = pytest.mark.gpu
 
-TAU = {"fp32": 2e-4, "fp16": 3e-2}
+TAU = {"fp32": 2e-5, "fp16": 1e-2}
 NWIN = 20
 
 
@@ -35,6 +36,16 @@ def _steps(name):
 
 def _eot(m):
     return 50257 if m.is_multilingual else 50256
+
+
+def decisive_prefix(name, kind, tau):
+    """Steps of the reference's fixed-work trajectory before the first one whose top-2
+    logit margin is within 2 * tau * (top-32 range): with every logit inside the
+    teacher-forced bound tau * range, no earlier choice can flip."""
+    gs = _steps(name)
+    topv = gs[f"tf_{kind}_topv"][:, 0]
+    close = (topv[:, 0] - topv[:, 1]) <= 2 * tau * (topv[:, 0] - topv[:, -1])
+    return int(np.argmax(close)) if close.any() else len(topv)
 
 
 @pytest.mark.parametrize("name", ["turbo", "large-v3"])
@@ -111,12 +122,13 @@ def _teacher_force(m, gs, kind, n_win):
 @pytest.mark.parametrize("n_win", [1, NWIN])
 @pytest.mark.parametrize("kind", ["beam_fixed", "greedy_fixed"])
 @pytest.mark.parametrize("dtype", ["fp16", "fp32"])
-@pytest.mark.parametrize("name", ["turbo", "large-v3"])
+@pytest.mark.parametrize("name", ["micro", "tiny.en", "turbo", "large-v3"])
 def test_teacher_forced_step_logits(name, dtype, kind, n_win):
     """Per-step logit tolerance along the reference's own fixed-work trajectory, all
     224 steps, at 1 window and at the bench batch (20 windows)."""
     gs = _steps(name)
     m = full_model(name, dtype)
+    assert m.dtype == dtype
     m.ctx.mel_write(np.concatenate([golden_window(name)] * n_win, axis=1))
     m.ctx.encode([3000 * i for i in range(n_win)], [3000] * n_win)
     rel, top1 = _teacher_force(m, gs, kind, n_win)

@@ -94,11 +94,21 @@ def test_decode_tokens(micro, window_mel, key, opts):
         assert res.avg_logprob == pytest.approx(float(g[f"{key}_avg_logprob"]), abs=2e-3)
         assert res.no_speech_prob == pytest.approx(float(g[f"{key}_no_speech_prob"]), rel=2e-2, abs=1e-7)
     else:
-        # fp16: identical first tokens; report the agreement length
+        # fp16: equal through the decisive prefix where the reference recorded its
+        # per-step top-2 margins (greedy runs): every step whose margin exceeds twice
+        # the teacher-forced fp16 logit bound (test_gpu_batch.py, micro row); other
+        # runs: the first token, agreement length reported
+        from test_gpu_batch import TAU, _steps
         n = min(len(got), len(ref))
         agree = int(np.argmax(got[:n] != ref[:n])) if np.any(got[:n] != ref[:n]) else n
-        print(f"{key} fp16 agreement {agree}/{len(ref)}")
-        assert agree >= 1
+        need = 1
+        if f"{key}_margins" in g.files:
+            topv = _steps("micro")["tf_greedy_fixed_topv"][:, 0]
+            eps = TAU["fp16"] * float(np.median(topv[:, 0] - topv[:, -1]))
+            close = g[f"{key}_margins"] <= 2 * eps
+            need = int(np.argmax(close)) if close.any() else len(ref)
+        print(f"{key} fp16 agreement {agree}/{len(ref)} (required {need})")
+        assert agree >= min(need, n)
 
 
 @pytest.mark.parametrize("run,schedule", [("clip_beam", "auto"), ("clip_greedy", "auto"), ("seq_greedy", "auto"), ("seq_beam", "auto"),

@@ -8,7 +8,9 @@ Bars:
     1e-3;
   * fp16 context (production): first-step logits within 2% of the logit range
     (max abs error over the reference top-64 / (max - min) of those values),
-    identical top-1, and >= 4 of the reference top-5 in our top-5.
+    identical top-1, and >= 4 of the reference top-5 in our top-5; free-running
+    greedy equal through the decisive prefix (every step whose reference margin
+    exceeds twice the teacher-forced fp16 bound of test_gpu_batch.py).
 """
 import os
 
@@ -74,7 +76,11 @@ def test_fp32_tokens_exact(name, kind):
 
 @pytest.mark.parametrize("name", MODELS)
 def test_fp16_greedy_agreement(name):
+    """fp16 greedy (free running, fixed work) equals the reference through every step
+    whose reference top-2 margin exceeds twice the teacher-forced fp16 logit bound
+    (test_gpu_batch.TAU): up to there no choice can flip."""
     import whisper
+    from test_gpu_batch import TAU, decisive_prefix
     g = _golden(name)
     m = _model(name, "fp16")
     eot = 50257 if m.is_multilingual else 50256
@@ -82,7 +88,8 @@ def test_fp16_greedy_agreement(name):
     got, ref = np.asarray(res.tokens), g["greedy_fixed_tokens"]
     n = min(len(got), len(ref))
     agree = int(np.argmax(got[:n] != ref[:n])) if np.any(got[:n] != ref[:n]) else n
-    print(f"{name} fp16 greedy agreement {agree}/{len(ref)}; avg_logprob {res.avg_logprob:.4f} vs "
-          f"{float(g['greedy_fixed_avg_logprob']):.4f}")
+    need = min(decisive_prefix(name, "greedy_fixed", TAU["fp16"]), len(ref))
+    print(f"{name} fp16 greedy agreement {agree}/{len(ref)} (decisive prefix {need}); avg_logprob "
+          f"{res.avg_logprob:.4f} vs {float(g['greedy_fixed_avg_logprob']):.4f}")
     assert len(got) == len(ref)
-    assert agree >= 8
+    assert agree >= need

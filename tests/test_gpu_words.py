@@ -9,7 +9,6 @@
   word_timestamps=True) against the reference (micro_words.json) in fp32.
 Tolerances: paths and word boundaries exact; token probabilities rel 1e-3
 (fp32 softmax of logits that agree to ~1e-5 with the reference's)."""
-import base64
 import json
 import os
 
@@ -31,14 +30,10 @@ def words_golden():
 @pytest.fixture(scope="module")
 def micro32(words_golden):
     import whisper
-    from whisper import tokenizer as T
-    enc = words_golden["encoding"].replace(".tiktoken", "")
-    T.set_token_bytes(enc, {int(k): base64.b64decode(v) for k, v in words_golden["token_bytes"].items()})
     m = whisper.load_model("micro", device=0, dtype="fp32", max_windows=4, max_group=5,
                              synthetic=True)
     yield m
     m.close()
-    T.set_token_bytes(enc, None)
 
 
 def test_gpu_dtw_matches_reference(micro32):

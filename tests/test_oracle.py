@@ -119,13 +119,10 @@ def test_median_filter_oracle_against_reference():
 def test_word_split_matches_reference_alignment_words():
     """Product tokenizer word splitting (tokenizer.py:277-327 restated) reproduces the
     words/token groups of the reference's find_alignment (micro_words.json)."""
-    import base64
     from whisper import tokenizer as T
     with open(os.path.join(GOLDEN, "micro_words.json")) as f:
         gw = json.load(f)
-    enc = gw["encoding"].replace(".tiktoken", "")
-    T.set_token_bytes(enc, {int(k): base64.b64decode(v) for k, v in gw["token_bytes"].items()})
-    try:
+    if True:  # the shipped rank file (whisper/assets/multilingual.tiktoken)
         tok = T.get_tokenizer(True, num_languages=S.MODEL_DIMS["micro"]["n_vocab"] - 51765 - 1, language="en",
                               task="transcribe")
         for case in gw["find_alignment"].values():
@@ -138,5 +135,3 @@ def test_word_split_matches_reference_alignment_words():
             assert len(ref) == len(words) - 1
             assert [w["word"] for w in ref] == words[:-1]
             assert [w["tokens"] for w in ref] == word_tokens[:-1]
-    finally:
-        T.set_token_bytes(enc, None)
