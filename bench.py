@@ -1,17 +1,21 @@
 #!/usr/bin/env python
 """xRT benchmark: large-v3, beam 5, fp16, synthetic audio, 1..8 MI355X (one process per GPU).
 
-A "step" is one ``transcribe()`` of the rank's audio shard (config 3 of
-BASELINE.json: 10 minutes of 16 kHz audio per GPU, weak scaling), in the
-sharded schedule of SURVEY.md §8(e): 30 s clip grid, condition_on_previous_text
-= False, temperature 0 — every clip's windows are batched through the encoder
-and the hipGraph decoder together.  The audio is resident in HBM before the
-timed region (``HipContext.audio_upload``); the only cross-rank exchanges are
-an all-reduce MAX of the log-mel global maximum (audio.py:155 is a whole-file
-max) and the final gather of the segment records, both over RCCL.
+A "step" is one ``transcribe()`` of a file through the multi-GPU path of SURVEY.md
+§8(e) (whisper/distributed.py): every rank computes the log-mel of its block of 30 s
+clips from the audio resident in its HBM, the log-mel maximum is all-reduced (MAX,
+RCCL), each rank decodes its clips (batched schedule: all its windows through the
+encoder and the hipGraph decoder step together), and the segment records are gathered
+on rank 0.  condition_on_previous_text = False, temperature 0.
 
-value = (audio seconds of all ranks x steps) / (max over ranks of the timed wall
-time) = whole-job xRT.  rank 0 prints one JSON line.
+Default (weak scaling, BASELINE config 3 at N = 1): the file holds ``--seconds``
+(600) of audio per rank.  ``--sharded-file 1`` (config 4): one file of ``--seconds``
+(e.g. 3600) in total, whatever the rank count (strong scaling).  With more than one
+rank, rank 0 re-transcribes the whole file unsharded after the timed region and
+reports whether the merged segments equal it (``verify``).
+
+value = (audio seconds of the whole file x steps) / (max over ranks of the timed
+wall time) = whole-job xRT.  rank 0 prints one JSON line.
 """
 
 import argparse
@@ -36,12 +40,20 @@ def parse():
     p.add_argument("--steps", type=int, default=3)
     p.add_argument("--warmup", type=int, default=1)
     p.add_argument("--model", default="large-v3")
-    p.add_argument("--seconds", type=float, default=600.0, help="audio seconds per GPU")
+    p.add_argument("--seconds", type=float, default=600.0,
+                   help="audio seconds per GPU (weak scaling); with --sharded-file, of the whole file")
+    p.add_argument("--sharded-file", type=int, default=0,
+                   help="config 4: one file of --seconds sharded over the ranks (strong scaling)")
+    p.add_argument("--verify", type=int, default=-1,
+                   help="rank 0 compares the merged segments with an unsharded run (default: when > 1 rank)")
+    p.add_argument("--latency", type=int, default=1,
+                   help="also time single-window decoding (1 window x beam: the per-token p50 of §8(d))")
     p.add_argument("--beam", type=int, default=5)
     p.add_argument("--dtype", default="fp16")
     p.add_argument("--max-windows", type=int, default=20)
     p.add_argument("--cpu-baseline", type=int, default=1)
-    p.add_argument("--cpu-steps", type=int, default=6, help="decoder steps in the CPU baseline sample")
+    p.add_argument("--cpu-steps", type=int, default=0,
+                   help="CPU baseline: beam decoder steps of its window (0 = the whole 224-step window)")
     p.add_argument("--dump", default="", help="write the last step's segments (tokens, avg_logprob) as JSON")
     p.add_argument("--word-timestamps", type=int, default=0,
                    help="config 5: transcribe(word_timestamps=True) (alignment + DTW on the GPU per window)")
@@ -107,12 +119,14 @@ def load_traffic(kernel):
     """HBM bytes per launch of `kernel` from the committed PMC pass
     (profiles/<round>/traffic.json, written by profiles/pmc_traffic.py: FETCH_SIZE x2
     + WRITE_SIZE per the gfx950 correction of MI355X_MICROARCH.md), or None."""
-    path = os.path.join(REPO, "profiles", "r01", "traffic.json")
-    try:
-        with open(path) as f:
-            return json.load(f)[kernel]["hbm_bytes_per_launch"]
-    except (OSError, KeyError, ValueError):
-        return None
+    for rnd in ("r02", "r01"):
+        path = os.path.join(REPO, "profiles", rnd, "traffic.json")
+        try:
+            with open(path) as f:
+                return json.load(f)[kernel]["hbm_bytes_per_launch"]
+        except (OSError, KeyError, ValueError):
+            continue
+    return None
 
 
 def encoder_flops(dims):
@@ -123,9 +137,11 @@ def encoder_flops(dims):
 
 
 def cpu_baseline(model_name, sd, audio, beams, n_steps):
-    """The oracle (CPU fp32 restatement, oracle/ref_whisper.py) on a bounded sample of
-    one 30 s window: encoder + first pass + n_steps beam decoder steps, extrapolated
-    to the 224-step fixed work of a window."""
+    """The oracle (CPU fp32 restatement, oracle/ref_whisper.py) decoding one 30 s window
+    exactly as the reference's DecodingTask does (encoder, first pass, then every
+    beam-search step with its filters, top-k candidate merge and KV reorder) with
+    fixed work (EOT suppressed: 224 steps).  n_steps > 0 stops after that many
+    steps and scales the step part to 224 (a bounded sample)."""
     import torch
     from oracle import ref_whisper as R
     from whisper import synthetic as S
@@ -137,30 +153,24 @@ def cpu_baseline(model_name, sd, audio, beams, n_steps):
     t0 = time.time()
     xa = m.encode(mel)
     t_enc = time.time() - t0
-    m.set_audio(xa)
-    toks = torch.tensor([list(st.sot_sequence)] * beams)
+    opts = R.Options(beam_size=beams, suppress_tokens=f"-1,{st.eot}", sample_len=n_steps or None)
     t0 = time.time()
-    logits, cache, _ = m.decoder_forward(toks, 0, None)
-    t_pre = time.time() - t0
-    offset = toks.shape[1]
-    nxt = logits[:, -1].argmax(-1, keepdim=True)
-    t0 = time.time()
-    for _ in range(n_steps):
-        logits, cache, _ = m.decoder_forward(nxt, offset, cache)
-        offset += 1
-        nxt = logits[:, -1].argmax(-1, keepdim=True)
-    t_step = (time.time() - t0) / n_steps
-    per_window = t_enc + t_pre + 224 * t_step
+    res = R.decode(m, mel, opts, st, xa=xa)
+    t_dec = time.time() - t0
+    steps = n_steps or 224
+    per_window = t_enc + t_dec * (224 / steps)
+    kind = "the whole window" if not n_steps else f"{steps} steps scaled to 224"
     return dict(value=round(30.0 / per_window, 4), unit="xRT (audio-s/s)", cores=threads, kind="port",
-                sample=f"1 window of {model_name}: encoder {t_enc:.2f}s + first pass {t_pre:.2f}s + "
-                       f"{n_steps} beam-{beams} steps at {t_step*1e3:.0f} ms/step, extrapolated to 224 steps "
-                       f"(oracle/ref_whisper.py, torch CPU fp32, {threads} threads)")
+                sample=f"1 window (30 s) of {model_name}, beam {beams}, {kind}: encoder {t_enc:.1f} s + decode "
+                       f"{t_dec:.1f} s ({len(res.tokens)} tokens; oracle/ref_whisper.py decode with the reference's "
+                       f"beam search, torch CPU fp32, {threads} threads)")
 
 
 def main():
     args = parse()
     world, rank, local, pg = dist_setup(args)
     import whisper
+    from whisper import distributed as D
     from whisper import synthetic as S
 
     dims = S.MODEL_DIMS[args.model]
@@ -173,30 +183,27 @@ def main():
     if not (rank == 0 and world == 1 and args.cpu_baseline):
         del sd
         sd = None
-    n_clips = int(round(args.seconds / 30.0))
-    # start,end pairs of a 30 s grid covering the whole shard (transcribe.py:172-181)
-    clip_ts = ",".join(f"{30 * i},{30 * (i + 1)}" for i in range(n_clips))
-    # the rank's shard of one long synthetic file (seeded per rank)
-    audio = S.synthetic_audio(args.seconds, seed=1000 + rank)
+    if args.word_timestamps and world > 1:
+        raise SystemExit("--word-timestamps is a single-GPU workload (config 5): sharding refuses it")
+    file_seconds = args.seconds if args.sharded_file else args.seconds * world
+    n_clips = int(round(file_seconds / 30.0))
+    # one seeded file, resident in every rank's HBM before the timed region
+    audio = S.synthetic_audio(file_seconds, seed=1000)
     dev_audio = model.ctx.audio_upload(audio)
-
-    def reduce_max(x):
-        return allreduce_max(pg, x)
-
-    if args.word_timestamps:
-        # word splitting needs token bytes; the box has no BPE rank file, so every text
-        # id decodes to its own word " w<id>" (host-side grouping only: the GPU work,
-        # first pass + alignment + DTW per window, is the same for any byte table)
-        from whisper import tokenizer as T
-        T.set_token_bytes("multilingual" if model.is_multilingual else "gpt2",
-                          {i: b" w%d" % i for i in range(dims["n_vocab"])})
+    decode_kw = dict(temperature=0.0, beam_size=args.beam, language="en")
 
     def one_step():
-        # per-rank log-mel, global max over ranks (all-reduce MAX), normalize, transcribe
-        return whisper.transcribe(model, dev_audio, temperature=0.0, beam_size=args.beam, language="en",
-                                  condition_on_previous_text=False, clip_timestamps=clip_ts,
-                                  mel_max_reduce=reduce_max if pg is not None else None, schedule="batched",
-                                  word_timestamps=bool(args.word_timestamps))
+        if args.word_timestamps:
+            # config 5 on one GPU: the same clip grid, words aligned on the GPU per window
+            clip_ts = ",".join(f"{30 * i},{30 * (i + 1)}" for i in range(n_clips))
+            return whisper.transcribe(model, dev_audio, condition_on_previous_text=False, clip_timestamps=clip_ts,
+                                      schedule="batched", word_timestamps=True, **decode_kw)["segments"]
+        st = D.prepare_shard(model, dev_audio, rank, world)
+        g = allreduce_max(pg, st.local_max)
+        segs = D.run_shard(model, st, g, **decode_kw)
+        if pg is None:
+            return D.merge_segments([segs])
+        return D.gather_segments(segs)  # rank 0: the merged file; others: None
 
     for _ in range(args.warmup):
         one_step()
@@ -213,35 +220,48 @@ def main():
     elapsed = time.perf_counter() - t0
     st1 = model.ctx.stats()
     elapsed_max = allreduce_max(pg, elapsed)
+    merged = results[-1]
 
     if args.dump and rank == 0:
         with open(args.dump, "w") as f:
-            json.dump([{k: s[k] for k in ("seek", "tokens", "avg_logprob", "no_speech_prob")}
-                       for s in results[-1]["segments"]], f)
+            json.dump([{k: s[k] for k in ("seek", "tokens", "avg_logprob", "no_speech_prob")} for s in merged], f)
 
-    # segment gather to rank 0 (the only data-path exchange besides the mel max)
-    seg_tokens = sum(len(s["tokens"]) for s in results[-1]["segments"])
-    n_segments = len(results[-1]["segments"])
-    if pg is not None:
-        gathered = [None] * world
-        pg.all_gather_object(gathered, (n_segments, seg_tokens))
-    else:
-        gathered = [(n_segments, seg_tokens)]
+    verify = None
+    if (args.verify if args.verify >= 0 else world > 1) and rank == 0:
+        # the whole file on this GPU alone, same options, unsharded: the merged records must equal it
+        clip_ts = ",".join(f"{30 * i},{30 * (i + 1)}" for i in range(n_clips))
+        ref = whisper.transcribe(model, audio, condition_on_previous_text=False, clip_timestamps=clip_ts,
+                                 schedule="batched", **decode_kw)["segments"]
+        same = [a["tokens"] == b["tokens"] and a["seek"] == b["seek"] for a, b in zip(merged, ref)]
+        verify = {"segments": len(merged), "unsharded_segments": len(ref),
+                  "equal": len(merged) == len(ref) and all(same),
+                  "segments_equal_frac": round(sum(same) / max(len(ref), 1), 4)}
 
+    seg_tokens = sum(len(s["tokens"]) for s in merged) if merged is not None else 0
     steps_done = st1["steps"] - st0["steps"]
     steps_ms = st1["steps_ms"] - st0["steps_ms"]
     enc_ms = st1["encode_ms"] - st0["encode_ms"]
     enc_windows = st1["encode_windows"] - st0["encode_windows"]
     ms_per_token = steps_ms / max(steps_done, 1)
-
+    per_rank_windows = -(-n_clips // world)
+    n_win = min(args.max_windows, per_rank_windows)
     # p50 per-token decode ms: median over the timed region's decode_steps chunks
     tok = model.ctx.token_ms()
     p50_token_ms = float(np.median(tok)) if len(tok) else ms_per_token
 
+    # overall roofline: the encoder's flops at the dense fp16 MFMA peak plus
+    # every decoder step's bytes at the HBM peak, over the measured wall time
+    mean_ctx = 3 + 112  # mid-window self-KV length for the byte count
+    ideal_s = (encoder_flops(dims) * enc_windows / (MFMA_F16_PEAK_TFS * 1e12)
+               + steps_done * decoder_step_bytes(dims, n_win, args.beam, mean_ctx) / (HBM_PEAK_GBS * 1e9))
+    overall = {"ideal_ms_per_step": round(ideal_s * 1e3 / args.steps, 2),
+               "frac": round(ideal_s / elapsed, 4),
+               "model": "encoder flops / 2.5 PFLOP/s + decoder step bytes (weights + cross-KV + self-KV at "
+                        "mean context 115) / 8 TB/s, rank-local"}
+
     # roofline of the dominant kernel (k_proj: the split-K projections of the decoder
-    # step, ~31% of step time over its three tile variants), timed live with HIP events on the context's
-    # stream over launches at the bench batch (all layers, so weights stream from HBM)
-    n_win = min(args.max_windows, n_clips)
+    # step), timed live with HIP events on the context's stream over launches at the
+    # bench batch (all layers, so weights stream from HBM)
     model.ctx.encode([3000 * i for i in range(n_win)], [3000] * n_win)
     from whisper.decoding import DecodingTask
     task = DecodingTask(model, whisper.DecodingOptions(language="en", beam_size=args.beam))
@@ -256,34 +276,55 @@ def main():
     xattn_ms = model.ctx.time_stage(3, 3)
     xattn_bytes = cross_attn_bytes_per_launch(dims, n_win, rows)
     step_ms = model.ctx.time_stage(0, 20)
-    mean_ctx = 3 + 112  # mid-window self-KV length for the byte count
     step_bytes = decoder_step_bytes(dims, n_win, args.beam, mean_ctx)
+
+    # single-window decoding (§8(d)'s p50: one _main_loop iteration at B = beam): one
+    # window, the whole 224-step fixed-work decode through decode_steps, per-token wall
+    # time of each 8-step chunk (graph launches + the host's done poll)
+    latency = None
+    if args.latency:
+        model.ctx.encode([0], [3000])
+        t1 = DecodingTask(model, whisper.DecodingOptions(language="en", beam_size=args.beam,
+                                                         suppress_tokens=f"-1,{task.tokenizer.eot}"))
+        model.ctx.decode_begin(t1.wh_opts(), [t1.initial_tokens], [t1.sot_index])
+        model.ctx.token_ms(reset=True)
+        model.ctx.decode_steps(t1.sample_len)
+        tk1 = model.ctx.token_ms(reset=True)
+        step1 = model.ctx.time_stage(0, 20)
+        latency = {"p50_token_ms_1window": round(float(np.median(tk1)), 4), "step_graph_ms_1window": round(step1, 4),
+                   "step_bytes_1window": decoder_step_bytes(dims, 1, args.beam, mean_ctx),
+                   "roofline_frac_1window": round(decoder_step_bytes(dims, 1, args.beam, mean_ctx) /
+                                                  (step1 * 1e-3) / (HBM_PEAK_GBS * 1e9), 4)}
 
     def gbs(b, ms):
         return b / (ms * 1e-3) / 1e9
 
     traffic = load_traffic("k_proj")
+    parallel = (f"one {file_seconds:.0f} s file sharded over {world} GPU(s) by 30 s clips (whisper/distributed.py): "
+                f"RCCL all-reduce(max) of the log-mel maximum + gather of the segment records")
     out = {
         "metric": "xRT (audio-s/s) large-v3 beam=5 @1/2/4/8 GPU; p50 per-token decode ms",
-        "value": round(world * args.seconds * args.steps / elapsed_max, 3),
+        "value": round(file_seconds * args.steps / elapsed_max, 3),
         "unit": "audio-s/s",
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": round(elapsed_max * 1e3 / args.steps, 2),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if args.sharded_file else "weak",
         "vs_baseline": None,
         "dtype": "fp16" if args.dtype == "fp16" else "f32",
         "data": "synthetic: seeded N(0,0.1^2)+440 Hz audio, seeded random-init weights at real dims",
-        "config": {"workload": f"{args.model} beam={args.beam} transcribe(), {args.seconds:.0f} s audio per GPU, "
+        "config": {"workload": f"{args.model} beam={args.beam} transcribe() of one {file_seconds:.0f} s file, "
                                f"30 s clip grid, condition_on_previous_text=False, temperature=0"
                                + (", word_timestamps=True" if args.word_timestamps else ""),
-                   "model": args.model, "global_batch": n_clips * world, "seq_len": 448,
-                   "parallelism": f"windows sharded over {world} GPU(s), RCCL all-reduce(max)+gather"},
-        "p50_token_ms": round(p50_token_ms, 4),
-        "mean_token_ms": round(ms_per_token, 4),
-        "tokens_per_window": round(gathered[0][1] / max(1, n_clips), 1),
+                   "model": args.model, "global_batch": n_clips, "seq_len": 448, "parallelism": parallel},
+        # §8(d): one _main_loop iteration at B = beam for a single window; the batch
+        # figures are the same per-token wall time with every window of the rank decoding
+        "p50_token_ms": latency["p50_token_ms_1window"] if latency else round(p50_token_ms, 4),
+        "p50_token_ms_batch": round(p50_token_ms, 4),
+        "mean_token_ms_batch": round(ms_per_token, 4),
+        "tokens_per_window": round(seg_tokens / max(1, n_clips), 1) if rank == 0 else None,
         "encoder_ms_per_window": round(enc_ms / max(enc_windows, 1), 3),
         "encoder_tflops": round(encoder_flops(dims) * enc_windows / (enc_ms * 1e-3) / 1e12, 1) if enc_ms else None,
         "roofline": {"bound": "hbm", "kernel": f"k_proj split-K projection ({rows} rows, avg of the six "
@@ -293,6 +334,7 @@ def main():
                      "traffic": traffic, "bytes_per_launch": gemv_bytes, "ms_per_launch": round(gemv_ms, 5),
                      "timing": "HIP events around each launch inside eager decoder steps",
                      "ms_per_launch_back_to_back": round(gemv_b2b_ms, 5)},
+        "roofline_overall": overall,
         "roofline_cross_attn": {"bound": "hbm", "kernel": f"k_cross_attn1 ({n_win} windows x {args.beam} beams)",
                                 "achieved": round(gbs(xattn_bytes, xattn_ms), 1), "peak": HBM_PEAK_GBS,
                                 "frac": round(gbs(xattn_bytes, xattn_ms) / HBM_PEAK_GBS, 4),
@@ -302,6 +344,10 @@ def main():
                           "frac": round(gbs(step_bytes, step_ms) / HBM_PEAK_GBS, 4),
                           "bytes_per_launch": step_bytes, "ms_per_launch": round(step_ms, 4)},
     }
+    if latency:
+        out["latency_1window"] = latency
+    if verify is not None:
+        out["verify"] = verify
     if rank == 0 and world == 1 and args.cpu_baseline and sd is not None:
         try:
             out["cpu_baseline"] = cpu_baseline(args.model, sd, audio, args.beam, args.cpu_steps)

@@ -89,3 +89,14 @@ def test_gloo_world2_collectives():
     assert out[1][1] is None
     assert [s["id"] for s in out[0][1]] == [0, 1, 2]
     assert [s["tokens"] for s in out[0][1]] == [[0, 0], [1, 0], [1, 1]]
+
+
+@pytest.mark.parametrize("opt", [dict(word_timestamps=True), dict(initial_prompt="hello"),
+                                 dict(carry_initial_prompt=True)])
+def test_run_shard_rejects_cross_window_state(opt):
+    """Options whose reference semantics carry state from window to window across a
+    rank boundary are refused rather than silently diverging (distributed.py header)."""
+    st = D.ShardState(rank=1, world=2, n_samples=0, total_frames=0, clips=[(0, 3000)], frame0=0, count=0,
+                      local_max=0.0)
+    with pytest.raises(ValueError):
+        D.run_shard(object(), st, 0.0, language="en", **opt)

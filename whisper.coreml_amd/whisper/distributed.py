@@ -17,6 +17,13 @@ scalar, the log-mel maximum (audio.py:155).  Each rank therefore
 The two phases are exposed separately (``prepare_shard`` / ``run_shard``) so one
 GPU can replay several ranks in turn, which is how the tests check that a sharded
 run equals the unsharded one.
+
+Two options would carry state across a rank boundary, so ``run_shard`` rejects them
+instead of diverging from the reference: ``word_timestamps`` (each window's first-word
+truncation reads the running ``last_speech_timestamp`` of the windows before it,
+timing.py:337 / transcribe.py:485-486) and ``initial_prompt`` (the reference gives it
+to the first window that is not skipped as silence, transcribe.py:299-321, which a
+rank cannot know before the earlier ranks have decoded).
 """
 from dataclasses import dataclass
 from typing import Callable, List, Optional, Sequence, Tuple
@@ -93,6 +100,9 @@ def run_shard(model, state: ShardState, global_max: float, audio=None, **transcr
     (batched schedule).  ``audio`` re-supplies host audio when the context's mel
     buffer was reused by another shard since ``prepare_shard``."""
     from .transcribe import transcribe
+    for key in ("word_timestamps", "initial_prompt", "carry_initial_prompt"):
+        if transcribe_kw.get(key):
+            raise ValueError(f"sharded transcription does not support {key} (it carries state across windows)")
     if not state.clips:
         return []
     if audio is not None:
@@ -101,8 +111,6 @@ def run_shard(model, state: ShardState, global_max: float, audio=None, **transcr
     model.ctx.mel_normalize(global_max)
     kw = dict(transcribe_kw)
     kw.update(condition_on_previous_text=False, clip_timestamps=seconds_csv(state.clips), schedule="batched")
-    if state.rank != 0:
-        kw.pop("initial_prompt", None)  # only the file's first window sees it
     out = transcribe(model, None, _mel_prepared=(state.total_frames, state.frame0, state.count), **kw)
     return out["segments"]
 
