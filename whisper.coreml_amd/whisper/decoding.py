@@ -208,17 +208,8 @@ def run_windows(model: "Whisper", options: DecodingOptions, prompts: Sequence[Op
             audio_features=ctx.audio_features(slots[i] if slots is not None else i) if audio_features else None,
             language=lang, tokens=toks,
             text=text, avg_logprob=avg, no_speech_prob=raw["no_speech_prob"], temperature=options.temperature,
-            compression_ratio=compression_ratio(text) if text else _token_compression_ratio(toks)))
+            compression_ratio=compression_ratio(text)))
     return out
-
-
-def _token_compression_ratio(tokens: List[int]) -> float:
-    """compression_ratio on the token stream when no BPE table is available
-    to produce text (the fallback heuristic then still sees repetition)."""
-    if not tokens:
-        return 0.0
-    b = np.asarray(tokens, dtype=np.int32).tobytes()
-    return len(b) / len(zlib.compress(b)) / 2.0
 
 
 def decode(model: "Whisper", mel, options: DecodingOptions = DecodingOptions(), **kwargs
