@@ -116,6 +116,11 @@ WH_DEV void epilogue_store(const GemmArgs& a, int m, int gi, int ri, int n, floa
 
 template <typename T>
 int launch_gemm(const GemmArgs& a, int epi, hipStream_t st);
+// launch_gemm with the large-M tile chosen explicitly: 256 = k_gemm_256 where the shape
+// allows it, 128 = k_gemm_tile (tools/gemm_bench A/B; launch_gemm uses 256 unless
+// WHISPER_HIP_GEMM=128)
+template <typename T>
+int launch_gemm_tiles(const GemmArgs& a, int epi, int tile_sel, hipStream_t st);
 
 // decoder-step projections (k_proj, wh_proj.hip) into split-K partial slabs
 // out_f32[z][M][N]; returns 0 and the split count, or < 0 when no tile configuration

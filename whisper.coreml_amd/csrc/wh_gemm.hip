@@ -17,6 +17,7 @@
 #include "wh_gemm.h"
 
 #include <algorithm>
+#include <type_traits>
 #include <cstdlib>
 
 namespace wh {
@@ -141,6 +142,194 @@ __global__ __launch_bounds__(256, 2) void k_gemm_tile(GemmArgs a) {
         v += b;
       }
       epilogue_store<T, EPI>(a, m, gi, ri, n, v);
+    }
+  }
+}
+
+// ============================================================ 256x256 pipelined GEMM (fp16)
+// The encoder / cross-KV / conv2 GEMMs (M = 1500 x windows rows, N and K multiples of
+// 256 / 128).  Structure (cdna_hip_programming.md §5 "The 256² 8-phase template"):
+//   * 8 waves as 2 (M) x 4 (N); a wave owns a 128x64 output tile, acc[8][4] float4;
+//   * one K-tile (64) = 4 phases, each computing one 64x32 quadrant of the wave tile
+//     (16 MFMAs); phase order Q(0,0) Q(0,1) Q(1,1) Q(1,0), so a phase re-reads only the
+//     A or the B half its predecessor did not already hold;
+//   * operands reach LDS by global_load_lds (16 B per lane, no VGPR staging) in
+//     "stages": half of one operand's tile (128 rows x 64 k = 16 KB = 2 loads per wave),
+//     one stage issued per phase, up to 6 stages in flight, retired by ONE counted
+//     `s_waitcnt vmcnt` per K-tile — the loads stay in flight across the barriers, which
+//     are raw s_barriers (a __syncthreads() would drain them);
+//   * the two wave groups (M halves: waves 0-3 and 4-7, one of each per SIMD) run one
+//     barrier apart: while one group's MFMAs run, the other issues its LDS reads and
+//     stages;
+//   * LDS image of a stage: 16 subtiles of 16 rows x 32 k (1 KB), each with the
+//     st_16x32 swizzle (16 B chunk index ^= 2 on rows 8-15: conflict-free ds_read_b128),
+//     applied on the global SOURCE address of the lane-linear glds write and on the read.
+// Stage schedule (phase P = 4t + q of K-tile t, buffer t & 1; stage names SA0 SA1 SB0 SB1
+// = A/B halves read in phases {0} {2} {0,3} {1}):
+//   q0: SA1(t+1)   q1: SB0(t+1)   q2: SA0(t+2)   q3: SB1(t+2), then vmcnt(4)
+// Every stage lands >= 2 phases after the last read of the buffer half it overwrites
+// (WAR, both groups), and the vmcnt at q3 retires all of tile t+1 one phase before its
+// first read (RAW, a barrier of both groups in between).
+namespace g256 {
+constexpr int BM = 256, BN = 256, BK = 64;
+constexpr int STAGE = 16384;      // one stage: 16 subtiles x 1 KB
+constexpr int BUF = 4 * STAGE;    // SA0 SA1 SB0 SB1
+enum { SA0 = 0, SA1 = 1, SB0 = 2, SB1 = 3 };
+}  // namespace g256
+
+WH_DEV void raw_barrier() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("" ::: "memory");
+}
+
+WH_DEV void glds16(const char* src, char* lds) {
+  __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)(src),
+                                   (__attribute__((address_space(3))) void*)(lds), 16, 0, 0);
+}
+
+template <int EPI>
+__global__ __launch_bounds__(512, 1) void k_gemm_256(GemmArgs a) {
+  using namespace g256;
+  __shared__ __attribute__((aligned(1024))) char smem[2 * BUF];  // the kernel's only LDS object
+
+  const int ntn = a.N / BN;
+  const int ntm = (a.M + BM - 1) / BM;
+  const int bid = xcd_remap(blockIdx.x, ntm * ntn);
+  const int tm = bid / ntn, tn = bid % ntn;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wr = wave >> 2, wc = wave & 3;
+  const int r = lane & 15, g = lane >> 4;
+
+  // staging: in every stage this wave fills subtiles 2*wave (k 0-31) and 2*wave+1 (k 32-63)
+  // of its 16-row block; lane -> row lane>>2, source chunk inverse-swizzled
+  const int srow = lane >> 2;
+  const int schunk = (lane & 3) ^ ((lane >> 5) << 1);
+  const half_t* X = reinterpret_cast<const half_t*>(a.X);
+  const half_t* W = reinterpret_cast<const half_t*>(a.W);
+  const char* src[4];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    // SA_h block `wave`: rows wr' * 128 + h * 64 + j * 16 with wr' = wave >> 2, j = wave & 3
+    int m = m0 + (wave >> 2) * 128 + h * 64 + (wave & 3) * 16 + srow;
+    if (m >= a.M) m = a.M - 1;
+    const int gi = m / a.x_group_rows, ri = m - gi * a.x_group_rows;
+    src[SA0 + h] = reinterpret_cast<const char*>(X + (int64_t)gi * a.x_group_stride + (int64_t)ri * a.ldx) + schunk * 16;
+    // SB_h block `wave`: columns wc' * 64 + h * 32 + j * 16 with wc' = wave >> 1, j = wave & 1
+    const int n = n0 + (wave >> 1) * 64 + h * 32 + (wave & 1) * 16 + srow;
+    src[SB0 + h] = reinterpret_cast<const char*>(W + (int64_t)n * a.K) + schunk * 16;
+  }
+  auto stage = [&](int buf, int st, int kt) {
+    const char* s = src[st] + kt * (BK * 2);
+    char* d = smem + buf * BUF + st * STAGE + wave * 2048;
+    glds16(s, d);
+    glds16(s + 64, d + 1024);
+  };
+
+  // fragment reads: lane (r, g) reads row r, k-chunk g of a subtile, swizzled
+  const int roff = r * 64 + ((g ^ ((r >> 3) << 1)) << 4);
+  Frag<half_t> af[4][2], bf[2][2];
+  auto read_a = [&](int buf, int h) {
+    const char* base = smem + buf * BUF + (SA0 + h) * STAGE + wr * 8192 + roff;
+#pragma unroll
+    for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) af[mi][ks].v = *reinterpret_cast<const half8_t*>(base + (mi * 2 + ks) * 1024);
+  };
+  auto read_b = [&](int buf, int h) {
+    const char* base = smem + buf * BUF + (SB0 + h) * STAGE + wc * 4096 + roff;
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) bf[j][ks].v = *reinterpret_cast<const half8_t*>(base + (j * 2 + ks) * 1024);
+  };
+
+  float4_t acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = (float4_t){0.f, 0.f, 0.f, 0.f};
+
+  auto mfma_quadrant = [&](int mh, int nh) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) mfma_step(acc[mh * 4 + mi][nh * 2 + j], bf[j][ks], af[mi][ks]);
+    __builtin_amdgcn_s_setprio(0);
+  };
+
+  const int nk = a.K / BK;  // even, >= 2 (launcher)
+  // one K-tile from LDS buffer `buf` (compile-time), staging tiles t+1 / t+2
+  auto ktile = [&](auto bufc, int t) {
+    constexpr int buf = decltype(bufc)::value;
+    const bool s1 = t + 1 < nk, s2 = t + 2 < nk;
+    // q0: Q(0,0)
+    read_b(buf, 0);
+    read_a(buf, 0);
+    if (s1) stage(buf ^ 1, SA1, t + 1);
+    raw_barrier();
+    mfma_quadrant(0, 0);
+    raw_barrier();
+    // q1: Q(0,1)
+    read_b(buf, 1);
+    if (s1) stage(buf ^ 1, SB0, t + 1);
+    raw_barrier();
+    mfma_quadrant(0, 1);
+    raw_barrier();
+    // q2: Q(1,1)
+    read_a(buf, 1);
+    if (s2) stage(buf, SA0, t + 2);
+    raw_barrier();
+    mfma_quadrant(1, 1);
+    raw_barrier();
+    // q3: Q(1,0); retire tile t+1 before the barrier
+    read_b(buf, 0);
+    if (s2) {
+      stage(buf, SB1, t + 2);
+      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    raw_barrier();
+    mfma_quadrant(1, 0);
+    raw_barrier();
+  };
+
+  // prologue: tile 0 complete, SA0 / SB1 of tile 1 in flight
+  stage(0, SA0, 0);
+  stage(0, SB1, 0);
+  stage(0, SA1, 0);
+  stage(0, SB0, 0);
+  stage(1, SA0, 1);
+  stage(1, SB1, 1);
+  asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  raw_barrier();
+  if (wr == 1) raw_barrier();  // group 1 runs one barrier behind group 0
+  for (int t = 0; t < nk; t += 2) {
+    ktile(std::integral_constant<int, 0>(), t);
+    ktile(std::integral_constant<int, 1>(), t + 1);
+  }
+  if (wr == 0) raw_barrier();
+
+  // epilogue: lane holds Y[m = m0 + wr*128 + mi*16 + r][n = n0 + wc*64 + ni*16 + 4g .. +3]
+#pragma unroll
+  for (int mi = 0; mi < 8; ++mi) {
+    const int m = m0 + wr * 128 + mi * 16 + r;
+    if (m >= a.M) continue;
+    const int gi = m / a.x_group_rows, ri = m - gi * a.x_group_rows;
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni) {
+      const int n = n0 + wc * 64 + ni * 16 + 4 * g;
+      float4_t v = acc[mi][ni];
+      if (a.bias) v += load4f(a.bias + n);
+      epilogue_store<half_t, EPI>(a, m, gi, ri, n, v);
     }
   }
 }
@@ -366,11 +555,36 @@ int gemv_ksplit(int M, int N, int K, int max_z, int mt_block) {
 
 // ============================================================ launchers
 template <typename T>
+int launch_gemm_tiles(const GemmArgs& a, int epi, int tile_sel, hipStream_t st);
+
+template <typename T>
 int launch_gemm(const GemmArgs& a, int epi, hipStream_t st) {
+  static const int tile_sel = [] {  // WHISPER_HIP_GEMM=128 keeps the 128x128 kernel (A/B)
+    const char* e = getenv("WHISPER_HIP_GEMM");
+    return e ? atoi(e) : 256;
+  }();
+  return launch_gemm_tiles<T>(a, epi, tile_sel, st);
+}
+
+template <typename T>
+int launch_gemm_tiles(const GemmArgs& a, int epi, int tile_sel, hipStream_t st) {
   if (a.M <= 0) return 0;
   const bool big = a.M > 128 && (a.N % TBN) == 0 && (a.K % (TKB / (int)sizeof(T))) == 0 && epi != EPI_F32_COLS &&
                    epi != EPI_PARTIAL && a.x_rows == nullptr;
-  if (big) {
+  const bool t256 = big && sizeof(T) == 2 && tile_sel == 256 && a.M >= 256 && (a.N % g256::BN) == 0 &&
+                    (a.K % (2 * g256::BK)) == 0 && epi != EPI_QKV_DEC &&
+                    // below one 256-tile per CU the 128-tile grid fills the chip better
+                    // (tools/gemm_bench: one window, fc1: 0.035 vs 0.039 ms)
+                    ((a.M + g256::BM - 1) / g256::BM) * (a.N / g256::BN) >= 256;
+  if (t256) {
+    const int nwg = ((a.M + g256::BM - 1) / g256::BM) * (a.N / g256::BN);
+    switch (epi) {
+#define CASE(E) case E: k_gemm_256<E><<<nwg, 512, 0, st>>>(a); break;
+      CASE(EPI_STORE) CASE(EPI_STORE_GELU) CASE(EPI_RESID) CASE(EPI_GELU_POS) CASE(EPI_HEADSPLIT) CASE(EPI_QKV_ENC)
+#undef CASE
+      default: return -1;
+    }
+  } else if (big) {
     const int nwg = ((a.M + TBM - 1) / TBM) * (a.N / TBN);
     switch (epi) {
 #define CASE(E) case E: k_gemm_tile<T, E><<<nwg, 256, 0, st>>>(a); break;
@@ -462,6 +676,7 @@ int launch_gemm(const GemmArgs& a, int epi, hipStream_t st) {
 }
 
 template int launch_gemm<float>(const GemmArgs&, int, hipStream_t);
+template int launch_gemm_tiles<half_t>(const GemmArgs&, int, int, hipStream_t);
 template int launch_gemm<half_t>(const GemmArgs&, int, hipStream_t);
 
 }  // namespace wh
