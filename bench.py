@@ -99,11 +99,27 @@ def decoder_step_bytes(dims, n_windows, beams, mean_ctx, elem=2):
     return weights + cross + selfkv
 
 
+def p1_path(rows):
+    """The decoder step at <= 8 rows runs k_proj1 (whole-K projections with fused
+    LayerNorm prologues and epilogues: wh_runtime.hip dec_layers_p1) unless
+    WHISPER_HIP_P1=0; larger batches run the split-K k_proj."""
+    return rows <= 8 and os.environ.get("WHISPER_HIP_P1", "1") != "0"
+
+
 def projection_bytes_per_launch(dims, rows, elem=2):
-    """Algorithmic bytes of one split-K projection GEMV, averaged over the six per
+    """Algorithmic bytes of one decoder-step projection, averaged over the six per
     decoder layer (qkv n->3n, out n->n, cross-q n->n, cross-out n->n, fc1 n->4n,
-    fc2 4n->n): weights N*K + activations rows*K (fp16) + fp32 result rows*N."""
+    fc2 4n->n).  Split-K k_proj: weights N*K + activations rows*K (fp16) + fp32 result
+    rows*N.  k_proj1 (p1_path): weights N*K; the LayerNorm'd projections read the fp32
+    residual rows*K*4 + gamma/beta and write rows*N fp16; the residual ones read
+    rows*K fp16 and read + write the fp32 residual rows*N*4*2."""
     n = dims["n_text_state"]
+    if p1_path(rows):
+        ln = [(3 * n, n), (n, n), (4 * n, n)]
+        res = [(n, n), (n, n), (n, 4 * n)]
+        tot = sum(N * K * elem + rows * K * 4 + 2 * K * 4 + rows * N * elem for N, K in ln)
+        tot += sum(N * K * elem + rows * K * elem + rows * N * 8 for N, K in res)
+        return tot // 6
     shapes = [(3 * n, n), (n, n), (n, n), (n, n), (4 * n, n), (n, 4 * n)]
     tot = sum(N * K * elem + rows * K * elem + rows * N * 4 for N, K in shapes)
     return tot // len(shapes)
@@ -299,7 +315,7 @@ def main():
     def gbs(b, ms):
         return b / (ms * 1e-3) / 1e9
 
-    traffic = load_traffic("k_proj")
+    traffic = load_traffic("k_proj1" if p1_path(rows) else "k_proj")
     parallel = (f"one {file_seconds:.0f} s file sharded over {world} GPU(s) by 30 s clips (whisper/distributed.py): "
                 f"RCCL all-reduce(max) of the log-mel maximum + gather of the segment records")
     out = {
@@ -327,8 +343,9 @@ def main():
         "tokens_per_window": round(seg_tokens / max(1, n_clips), 1) if rank == 0 else None,
         "encoder_ms_per_window": round(enc_ms / max(enc_windows, 1), 3),
         "encoder_tflops": round(encoder_flops(dims) * enc_windows / (enc_ms * 1e-3) / 1e12, 1) if enc_ms else None,
-        "roofline": {"bound": "hbm", "kernel": f"k_proj split-K projection ({rows} rows, avg of the six "
-                                                f"per decoder layer)",
+        "roofline": {"bound": "hbm", "kernel": (f"k_proj1 whole-K projection, fused LayerNorm / epilogue ({rows} rows"
+                                                if p1_path(rows) else f"k_proj split-K projection ({rows} rows")
+                                               + ", avg of the six per decoder layer)",
                      "achieved": round(gbs(gemv_bytes, gemv_ms), 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(gbs(gemv_bytes, gemv_ms) / HBM_PEAK_GBS, 4),
                      "traffic": traffic, "bytes_per_launch": gemv_bytes, "ms_per_launch": round(gemv_ms, 5),

@@ -49,6 +49,11 @@ struct GemmArgs {
   const float* ln_g = nullptr;
   const float* ln_b = nullptr;
   float ln_eps = 1e-5f;
+  // k_proj1 in-launch split-K: fp32 slabs [ZS][N/16][256] and one arrival counter per
+  // 16-column tile (zero between launches: the last arriver re-arms it)
+  float* p1_slab = nullptr;
+  int* p1_cnt = nullptr;
+  int p1_slabs = 0;  // slab capacity (1 KB slabs) of p1_slab
 };
 
 template <typename T, int EPI>
@@ -130,6 +135,14 @@ template <typename T>
 // i.e. its execution time as a profiler sees it, with no marker packets around it
 int launch_proj_partial(const GemmArgs& a, int max_z, hipStream_t st, int* z_out, hipEvent_t ev0 = nullptr,
                         hipEvent_t ev1 = nullptr);
+
+// single-window decoder-step projections (k_proj1, wh_proj.h): <= 8 rows, fused
+// epilogue, optional LayerNorm prologue, in-launch split-K for the n-wide outputs;
+// proj1_supported(R, n): model width n has a configuration; launch returns -1 otherwise
+bool proj1_supported(int R, int n);
+template <typename T>
+int launch_proj1(const GemmArgs& a, int epi, bool ln, hipStream_t st, hipEvent_t ev0 = nullptr,
+                 hipEvent_t ev1 = nullptr);
 
 // split-K factor the skinny paths use for EPI_PARTIAL at this shape (<= min(16, max_z))
 int gemv_ksplit(int M, int N, int K, int max_z = 16, int mt_block = 0);

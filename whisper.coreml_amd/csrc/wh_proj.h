@@ -147,4 +147,194 @@ __global__ __launch_bounds__(64 * NSUB * KW) void k_proj(GemmArgs a) {
   }
 }
 
+// ------------------------------------------------------------ single-window step layer
+// k_proj1: the decoder-step projections at <= P1_RMAX rows (one window's beams: the
+// per-token latency path), with no separate reduction launch on either side:
+//  * prologue (CPL > 0): X = LayerNorm(x) of the fp32 residual rows, re-derived by every
+//    workgroup from the full rows (R x n x 4 B of L2 reads, one wave per row, CPL float4
+//    per lane) — replaces the k_resid_ln launch before the projection;
+//  * a workgroup owns NSUB x 16 output columns x a K range of KC = KW*NSTEP*32 (the
+//    k_proj tilings: <= 256 workgroups of 20-51 KB of weights); its KW waves split the
+//    range and are summed in LDS in fixed order;
+//  * ZS = K / KC > 1: the ZS waves that hold one 16-column tile's slices meet in an
+//    in-launch split-K reduction (cdna_hip_programming.md §5 "Projection GEMM at M =
+//    256" item 2, write-through form): fp32 1 KB slab stored sc1 by the wave, vmcnt(0),
+//    relaxed agent fetch_add on the tile's counter; the wave drawing ZS-1 re-arms the
+//    counter and sums the ZS slabs (sc1 loads) in slice order (deterministic for any
+//    arrival order);
+//  * epilogue owns every output element: bias + in-place residual add (EPI_RESID),
+//    GELU, or the decoder QKV scatter (q + self-KV rows).
+// A decoder layer is 8 launches instead of 12 (wh_runtime.hip dec_layers_p1).
+// Load order: LN rows / X fragments (L2) first, then the wave's weight fragments (HBM),
+// all issued before the first wait, so the LN math overlaps the weight stream.
+constexpr int P1_RMAX = 8;
+
+template <typename T, int NSUB, int KW, int NSTEP, int CPL>
+struct Proj1Shape {
+  static constexpr int KC = KW * NSTEP * 32;             // K per workgroup
+  static constexpr int XROW = KC * (int)sizeof(T) + 16;  // padded LDS row (bytes)
+  static constexpr int XBYTES = CPL ? P1_RMAX * XROW : 0;
+  static constexpr int RBYTES = (KW - 1) * NSUB * 64 * 16;
+  static constexpr int LDS = (XBYTES > RBYTES ? XBYTES : RBYTES) > 16 ? (XBYTES > RBYTES ? XBYTES : RBYTES) : 16;
+};
+
+template <typename T, int NSUB, int KW, int NSTEP, int ZS, int CPL, int EPI>
+__global__ __launch_bounds__(64 * NSUB * KW) void k_proj1(GemmArgs a) {
+  using P = Proj1Shape<T, NSUB, KW, NSTEP, CPL>;
+  constexpr bool LN = CPL > 0;
+  constexpr int NWV = NSUB * KW;
+  constexpr int RPW = (P1_RMAX + NWV - 1) / NWV;  // LayerNorm rows per wave
+  extern __shared__ __attribute__((aligned(16))) char xs[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = lane & 15, g = lane >> 4;
+  const int sub = wave % NSUB, kw = wave / NSUB;
+  const int R = a.M, K = a.K, kz = blockIdx.y;
+  const int tile = blockIdx.x * NSUB + sub;  // this wave's 16-column tile
+  const int n0 = tile * 16;
+  const int kb = kz * P::KC;               // this workgroup's K range [kb, kb + KC)
+  const int kw0 = kb + kw * NSTEP * 32;    // this wave's
+  const T* W = reinterpret_cast<const T*>(a.W);
+
+  // 1. activations (clamped addresses, no branch around a load)
+  const int CH = K / 4;  // LN: float4 chunks per residual row
+  float4_t xv[LN ? RPW : 1][LN ? CPL : 1], gv[LN ? CPL : 1], bv[LN ? CPL : 1];
+  Frag<T> xf[LN ? 1 : NSTEP];
+  if constexpr (LN) {
+#pragma unroll
+    for (int j = 0; j < RPW; ++j) {
+      const float* xr = a.xf32 + (int64_t)min(wave + NWV * j, R - 1) * K;
+#pragma unroll
+      for (int i = 0; i < CPL; ++i) xv[j][i] = load4f(xr + 4 * min(lane + 64 * i, CH - 1));
+    }
+#pragma unroll
+    for (int i = 0; i < CPL; ++i) {
+      const int c = min(lane + 64 * i, CH - 1);
+      gv[i] = load4f(a.ln_g + 4 * c);
+      bv[i] = load4f(a.ln_b + 4 * c);
+    }
+  } else {
+    const T* xp = reinterpret_cast<const T*>(a.X) + (int64_t)min(r, R - 1) * a.ldx + kw0 + 8 * g;
+#pragma unroll
+    for (int s = 0; s < NSTEP; ++s) frag_load(xf[s], xp + s * 32);
+  }
+  // 2. the wave's weight fragments: 16 columns x NSTEP k-steps
+  const T* wp = W + (int64_t)min(n0 + r, a.N - 1) * K + kw0 + 8 * g;
+  Frag<T> wf[NSTEP];
+#pragma unroll
+  for (int s = 0; s < NSTEP; ++s) frag_load_stream(wf[s], wp + s * 32);
+  // the epilogue's operands ride in the same round trip: bias (every k_proj1 call has
+  // one) and, for the residual add, this lane's x (only this tile's reducer writes it)
+  const int n = n0 + 4 * g, re = min(r, R - 1);
+  const float4_t pre_b = load4f(a.bias + n);
+  float4_t pre_x = (float4_t){0.f, 0.f, 0.f, 0.f};
+  if constexpr (EPI == EPI_RESID) pre_x = load4f(a.out_f32 + (int64_t)re * a.ldo + n);
+  // every load above is issued before any wait (else hipcc streams them through a
+  // sliding window of ~9, several round trips per wave)
+  __builtin_amdgcn_sched_barrier(0);
+
+  // 3. LayerNorm of the full rows (biased variance, two passes in registers: the
+  // arithmetic of k_layernorm); this workgroup's K range of it -> LDS
+  if constexpr (LN) {
+#pragma unroll
+    for (int j = 0; j < RPW; ++j) {
+      const int row = wave + NWV * j;
+      float s = 0.f;
+#pragma unroll
+      for (int i = 0; i < CPL; ++i)
+        if (lane + 64 * i < CH) s += xv[j][i][0] + xv[j][i][1] + xv[j][i][2] + xv[j][i][3];
+      const float mean = wave_sum(s) / (float)K;
+      float q = 0.f;
+#pragma unroll
+      for (int i = 0; i < CPL; ++i)
+        if (lane + 64 * i < CH) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float d = xv[j][i][e] - mean;
+            q += d * d;
+          }
+        }
+      const float rstd = rsqrtf(wave_sum(q) / (float)K + a.ln_eps);
+      if (row < R) {
+#pragma unroll
+        for (int i = 0; i < CPL; ++i) {
+          const int k = 4 * (lane + 64 * i) - kb;
+          if (k >= 0 && k < P::KC) {
+            const float4_t v = xv[j][i];
+            store4(reinterpret_cast<T*>(xs + row * P::XROW) + k, (v[0] - mean) * rstd * gv[i][0] + bv[i][0],
+                   (v[1] - mean) * rstd * gv[i][1] + bv[i][1], (v[2] - mean) * rstd * gv[i][2] + bv[i][2],
+                   (v[3] - mean) * rstd * gv[i][3] + bv[i][3]);
+          }
+        }
+      }
+    }
+    __syncthreads();
+  }
+
+  // 4. MFMAs in load order
+  float4_t acc = (float4_t){0.f, 0.f, 0.f, 0.f};
+  if constexpr (LN) {
+    const char* xl = xs + min(r, R - 1) * P::XROW + (kw * NSTEP * 32 + 8 * g) * (int)sizeof(T);
+#pragma unroll
+    for (int s = 0; s < NSTEP; ++s) {
+      Frag<T> x1;
+      frag_load(x1, reinterpret_cast<const T*>(xl + s * 32 * (int)sizeof(T)));
+      mfma_step(acc, wf[s], x1);
+    }
+  } else {
+#pragma unroll
+    for (int s = 0; s < NSTEP; ++s) mfma_step(acc, wf[s], xf[s]);
+  }
+
+  // 5. fixed-order sum of the KW wave tiles
+  if constexpr (KW > 1) {
+    if constexpr (LN) __syncthreads();  // xs is reused
+    float4_t* red = reinterpret_cast<float4_t*>(xs);  // [KW-1][NSUB][64]
+    if (kw > 0) red[((kw - 1) * NSUB + sub) * 64 + lane] = acc;
+    __syncthreads();
+    if (kw > 0) return;
+#pragma unroll
+    for (int q = 1; q < KW; ++q) acc += red[((q - 1) * NSUB + sub) * 64 + lane];
+  }
+
+  // 6. split-K: the column tile's ZS workgroups meet; the last to arrive sums the slabs
+  if constexpr (ZS > 1) {
+    // write-through form (cdna_hip_programming.md §6 Guideline 16 R1): the slab is stored
+    // sc1 and drained by its one storing wave, the counter add is a relaxed agent atomic,
+    // and the reducer reads every slab with sc1 loads, so neither side needs a fence
+    // (the plain-store + release / acquire form measured 2.5 us slower per launch)
+    typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+    const int ntile = gridDim.x * NSUB;
+    const auto rs = __builtin_amdgcn_make_buffer_rsrc(a.p1_slab, 0, 0x7fffffff, 0x00020000);
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc), rs, ((kz * ntile + tile) * 256 + lane * 4) * 4,
+                                           0, 16);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    int ticket = 0;
+    if (lane == 0) ticket = __hip_atomic_fetch_add(a.p1_cnt + tile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    ticket = __shfl(ticket, 0, 64);
+    if (ticket != ZS - 1) return;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // no instruction: keeps the loads below the add
+    if (lane == 0) __hip_atomic_store(a.p1_cnt + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    float4_t pv[ZS];  // every slab load issued before the first add; summed in slice order
+#pragma unroll
+    for (int s = 0; s < ZS; ++s)
+      pv[s] = __builtin_bit_cast(float4_t,
+                                 __builtin_amdgcn_raw_buffer_load_b128(rs, ((s * ntile + tile) * 256 + lane * 4) * 4, 0, 16));
+    acc = pv[0];
+#pragma unroll
+    for (int s = 1; s < ZS; ++s) acc += pv[s];
+  }
+
+  // 7. epilogue: lane holds Y[r][n0 + 4g .. +3]
+  if (r >= R) return;
+  acc += pre_b;
+  if constexpr (EPI == EPI_RESID) {
+    pre_x += acc;
+    store4(a.out_f32 + (int64_t)r * a.ldo + n, pre_x[0], pre_x[1], pre_x[2], pre_x[3]);
+  } else {
+    epilogue_store<T, EPI>(a, r, 0, r, n, acc);
+  }
+}
+
+// launch_proj1 (wh_gemm.h): a.M <= P1_RMAX rows; the configuration comes from the
+// model width (wh_proj.hip p1_launch); split tiles need a.p1_slab / a.p1_cnt
+
 }  // namespace wh

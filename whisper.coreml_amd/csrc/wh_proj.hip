@@ -119,6 +119,79 @@ int launch_proj_partial(const GemmArgs& a, int max_z, hipStream_t st, int* z_out
   return 0;
 }
 
+// ------------------------------------------------------------ k_proj1 (single-window step)
+// Configurations per model width n (S = n / 32 k-steps = BKW x NS), (nsub, kw, nstep, zs):
+//   qkv (n -> 3n) and cross-q (n -> n), LayerNorm prologue: (1, BKW, NS, 1), whole K;
+//   fc1 (n -> 4n), LayerNorm prologue: (F1SUB, BKW, NS, 1), whole K (32 columns per
+//     workgroup at n = 1280 in fp16: 160 workgroups; fp32 keeps 16, its 16-wave form spills);
+//   out, cross-out (n -> n, residual): (1, BKW / 2, NS, 2);  fc2 (4n -> n): (1, 2 BKW, NS, 2).
+// Measured at n = 1280 (large-v3, 5 rows, graph-mode rocprof, profiles/r02/p1_tilings.txt):
+// the in-launch reduction's cost grows with the split count — k_proj's own tilings with
+// 4-16 slices per tile took 6.6 / 10.3 / 9.3 / 8.1 / 7.5 us (nn / fc2 / fc1 / cross-q / qkv)
+// against 5.5 / 8.0 / 8.3 / 5.4 / 5.7 us for the tilings here, which split only the
+// residual projections, in two.
+namespace {
+template <typename T, int NSUB, int KW, int NS, int ZS, int CPL, int EPI>
+int p1_go(const GemmArgs& a, hipStream_t st, hipEvent_t ev0, hipEvent_t ev1) {
+  using P = Proj1Shape<T, NSUB, KW, NS, CPL>;
+  static_assert(P::LDS <= 64 * 1024, "k_proj1 LDS");
+  static_assert(NSUB * KW <= 16, "k_proj1 waves");
+  if (a.K != ZS * P::KC || a.N % (16 * NSUB)) return -1;
+  if (ZS > 1 && (!a.p1_slab || !a.p1_cnt || (int64_t)ZS * (a.N / 16) > a.p1_slabs)) return -1;
+  const dim3 grid(a.N / (16 * NSUB), ZS), block(64 * NSUB * KW);
+  void (*f)(GemmArgs) = &k_proj1<T, NSUB, KW, NS, ZS, CPL, EPI>;
+  if (ev0)
+    hipExtLaunchKernelGGL(f, grid, block, P::LDS, st, ev0, ev1, 0, a);
+  else
+    hipLaunchKernelGGL(f, grid, block, P::LDS, st, a);
+  return 0;
+}
+
+// one model width: the five kernels its step uses
+template <typename T, int CPL, int BKW, int NS, int F1SUB>
+int p1_width_launch(const GemmArgs& a, int epi, bool ln, int n, hipStream_t st, hipEvent_t e0, hipEvent_t e1) {
+  if (ln) {
+    if (a.K != n) return -1;
+    if (epi == EPI_QKV_DEC && a.N == 3 * n) return p1_go<T, 1, BKW, NS, 1, CPL, EPI_QKV_DEC>(a, st, e0, e1);
+    if (epi == EPI_STORE_GELU && a.N == 4 * n) return p1_go<T, F1SUB, BKW, NS, 1, CPL, EPI_STORE_GELU>(a, st, e0, e1);
+    if (epi == EPI_STORE && a.N == n) return p1_go<T, 1, BKW, NS, 1, CPL, EPI_STORE>(a, st, e0, e1);
+    return -1;
+  }
+  if (epi != EPI_RESID || a.N != n) return -1;
+  if (a.K == n) return p1_go<T, 1, BKW / 2, NS, 2, 0, EPI_RESID>(a, st, e0, e1);
+  if (a.K == 4 * n) return p1_go<T, 1, 2 * BKW, NS, 2, 0, EPI_RESID>(a, st, e0, e1);
+  return -1;
+}
+}  // namespace
+
+bool proj1_supported(int R, int n) {
+  if (R < 1 || R > P1_RMAX) return false;
+  switch (n) {
+    case 1280: case 1024: case 768: case 512: case 384: case 128: return true;
+    default: return false;
+  }
+}
+
+template <typename T>
+int launch_proj1(const GemmArgs& a, int epi, bool ln, hipStream_t st, hipEvent_t ev0, hipEvent_t ev1) {
+  if (a.M < 1 || a.M > P1_RMAX || a.N % 16 || !a.bias) return -1;
+  if (ln && (!a.xf32 || !a.ln_g || !a.ln_b)) return -1;
+  // the model width: the LayerNorm'd input (K) or the residual output (N)
+  const int n = ln ? a.K : a.N;
+  switch (n) {  //                            CPL BKW NS F1SUB
+    case 1280: return p1_width_launch<T, 5, 8, 5, sizeof(T) == 2 ? 2 : 1>(a, epi, ln, n, st, ev0, ev1);
+    case 1024: return p1_width_launch<T, 4, 8, 4, 1>(a, epi, ln, n, st, ev0, ev1);
+    case 768: return p1_width_launch<T, 3, 8, 3, 1>(a, epi, ln, n, st, ev0, ev1);
+    case 512: return p1_width_launch<T, 2, 8, 2, 1>(a, epi, ln, n, st, ev0, ev1);
+    case 384: return p1_width_launch<T, 2, 4, 3, 1>(a, epi, ln, n, st, ev0, ev1);
+    case 128: return p1_width_launch<T, 1, 4, 1, 1>(a, epi, ln, n, st, ev0, ev1);
+    default: return -1;
+  }
+}
+
+template int launch_proj1<float>(const GemmArgs&, int, bool, hipStream_t, hipEvent_t, hipEvent_t);
+template int launch_proj1<half_t>(const GemmArgs&, int, bool, hipStream_t, hipEvent_t, hipEvent_t);
+
 template int launch_proj_partial<float>(const GemmArgs&, int, hipStream_t, int*, hipEvent_t, hipEvent_t);
 template int launch_proj_partial<half_t>(const GemmArgs&, int, hipStream_t, int*, hipEvent_t, hipEvent_t);
 

@@ -183,6 +183,9 @@ struct Ctx : public wh_ctx {
   T *xn_d, *q_d, *att_d, *hm_d;
   int *row_tok, *row_pos, *row_win, *row_slot, *win_row0, *win_nrows, *win_slot, *rows_in, *src_rows;
   int *st_row_win, *st_row_slot, *st_win_row0, *st_win_nrows, *st_win_slot;
+  static constexpr int P1_SLABS = 2048;  // k_proj1 split-K slabs: zs x 16-column tiles <= 16 x 80 at n = 1280
+  float* p1_slab = nullptr;  // k_proj1 in-launch split-K slabs [zs][N/16][256]
+  int* p1_cnt = nullptr;     // and arrival counters [4n/16] (zero between launches)
   int* qk_map;  // [Ld][nh]
   unsigned* suppress;
   DecState S;
@@ -314,6 +317,7 @@ struct Ctx : public wh_ctx {
     addA((size_t)Wcap * Gcap * LP_SLICES * LP_REC * 4);
     addA(64);
     addA(64);
+    addA((size_t)P1_SLABS * 256 * 4); addA((size_t)(4 * n / 16) * 4);  // k_proj1 split-K slabs + counters
     HIPCHK(hipMalloc(&abase, ab));
     HIPCHK(hipMemset(abase, 0, ab));
     aa.base = (char*)abase;
@@ -346,7 +350,8 @@ struct Ctx : public wh_ctx {
     S.cand_val = fa((size_t)Wcap * Gcap * KC); S.cand_idx = ia((size_t)Wcap * Gcap * KC);
     S.lpart = fa((size_t)Wcap * Gcap * LP_SLICES * LP_REC);
     S.seed = (unsigned long long*)aa.take(64);
-    if (!S.seed || !S.cand_idx) return fail(-3, "activation arena overflow");
+    p1_slab = fa((size_t)P1_SLABS * 256); p1_cnt = ia(4 * n / 16);  // zeroed with the arena
+    if (!S.seed || !S.cand_idx || !p1_cnt) return fail(-3, "activation arena overflow");
     S.nw = Wcap; S.G = 1; S.ctx = CTX; S.hctx = HCTX; S.maxc = 16;
     HIPCHK(hipMalloc(&d_gmax, 64));
     d_gmax_f = (float*)(d_gmax + 4);
@@ -752,6 +757,8 @@ struct Ctx : public wh_ctx {
     // split-K into fp32 partial slabs; QKV's reduction is fused into self-attention
     const bool skinny = step && R <= 128;
     GemmArgs g;
+    if (step && !qkmap && p1_active(R))
+      return dec_layers_p1(R, rw, rs, rp, ancG, nwin, wr0, wnr, wsl);
     launch_layernorm<T>(x_d, xn_d, dec[0].ln1_g, dec[0].ln1_b, R, n, 1e-5f, nullptr, st);
     for (int l = 0; l < Ld; ++l) {
       auto& e = dec[l];
@@ -792,6 +799,118 @@ struct Ctx : public wh_ctx {
       const bool last = l + 1 == Ld;
       TRY(resid(hm_d, 4 * n, e.w2, e.b2, R, last ? ln_g : dec[l + 1].ln1_g, last ? ln_b : dec[l + 1].ln1_b));
     }
+    return 0;
+  }
+
+  // Decoder step at <= P1_RMAX rows (one window's beams: the per-token latency path):
+  // every projection is one k_proj1 launch over the whole K with its epilogue fused
+  // (QKV scatter, residual add, GELU) and the LayerNorm before it recomputed in its
+  // prologue, so a layer is 8 launches: qkv, self-attn, out, cross-q, cross-attn,
+  // cross-out, fc1, fc2 (12 on the split-K path: + 3 resid+LN, + reduce+GELU).
+  // WHISPER_HIP_P1=0 keeps the split-K path (A/B).
+  static bool p1_enabled() {
+    static const bool on = [] {
+      const char* e = getenv("WHISPER_HIP_P1");
+      return !(e && e[0] == '0');
+    }();
+    return on;
+  }
+
+  int p1(GemmArgs& g, int epi, bool ln) {
+    g.p1_slab = p1_slab;
+    g.p1_cnt = p1_cnt;
+    g.p1_slabs = P1_SLABS;
+    // time_stage(7): each projection of an eager step timed by its own dispatch events
+    const bool tev = proj_ev_n < (int)proj_ev.size() / 2;
+    const int rc = tev ? launch_proj1<T>(g, epi, ln, st, proj_ev[2 * proj_ev_n], proj_ev[2 * proj_ev_n + 1])
+                       : launch_proj1<T>(g, epi, ln, st);
+    if (tev && rc == 0) ++proj_ev_n;
+    return rc == 0 ? 0 : fail(-20, "k_proj1 launch failed code " + std::to_string(rc));
+  }
+
+  // the six projections of layer l as the step issues them (p1 path: k_proj1 with the
+  // step's epilogues; split path: k_proj into partial slabs) — time_stage(2)
+  int layer_projections(int l, int R) {
+    const int n = ns;
+    auto& e = dec[l];
+    if (p1_active(R)) {
+      GemmArgs g;
+      g.W = e.wqkv; g.bias = e.bqkv; g.M = R; g.N = 3 * n; g.K = n;
+      g.xf32 = x_d; g.ln_g = e.ln1_g; g.ln_b = e.ln1_b; g.ln_eps = 1e-5f;
+      g.out = q_d; g.ldo = n; g.hs_state = n; g.hs_heads = nh;
+      g.row_win = st_row_win; g.row_slot = st_row_slot; g.row_pos = row_pos; g.kc = kc[l]; g.vc = vc[l];
+      g.kv_beams = Gcap; g.kv_ctx = CTX;
+      TRY(p1(g, EPI_QKV_DEC, true));
+      struct Q { const T* X; int K; const T* W; const float* b; int N; int epi; const float* lg; const float* lb; T* out; };
+      const Q qs[5] = {{att_d, n, e.wo, e.bo, n, EPI_RESID, nullptr, nullptr, nullptr},
+                       {nullptr, n, e.wqx, e.bqx, n, EPI_STORE, e.lnx_g, e.lnx_b, q_d},
+                       {att_d, n, e.wox, e.box, n, EPI_RESID, nullptr, nullptr, nullptr},
+                       {nullptr, n, e.w1, e.b1, 4 * n, EPI_STORE_GELU, e.ln2_g, e.ln2_b, hm_d},
+                       {hm_d, 4 * n, e.w2, e.b2, n, EPI_RESID, nullptr, nullptr, nullptr}};
+      for (const Q& q : qs) {
+        g = GemmArgs();
+        g.W = q.W; g.bias = q.b; g.M = R; g.N = q.N; g.K = q.K;
+        if (q.lg) {
+          g.xf32 = x_d; g.ln_g = q.lg; g.ln_b = q.lb; g.ln_eps = 1e-5f; g.out = q.out; g.ldo = q.N;
+        } else {
+          g.X = q.X; g.ldx = q.K; g.out_f32 = x_d; g.ldo = n;
+        }
+        TRY(p1(g, q.epi, q.lg != nullptr));
+      }
+      return 0;
+    }
+    struct P { const T* X; int K; const T* W; int N; } ps[6] = {
+        {xn_d, n, e.wqkv, 3 * n}, {att_d, n, e.wo, n}, {xn_d, n, e.wqx, n},
+        {att_d, n, e.wox, n},     {xn_d, n, e.w1, 4 * n}, {hm_d, 4 * n, e.w2, n}};
+    for (auto& p : ps) {
+      int ks = 0;
+      TRY(partial(p.X, p.K, p.W, R, p.N, p.K, &ks));
+    }
+    return 0;
+  }
+
+  bool p1_active(int R) const { return p1_enabled() && proj1_supported(R, ns); }
+
+  int dec_layers_p1(int R, const int* rw, const int* rs, const int* rp, int ancG, int nwin, const int* wr0,
+                    const int* wnr, const int* wsl) {
+    const int n = ns;
+    for (int l = 0; l < Ld; ++l) {
+      auto& e = dec[l];
+      // self-attention block: q, k, v of LN1(x) (k / v straight into the cache)
+      GemmArgs g;
+      g.W = e.wqkv; g.bias = e.bqkv; g.M = R; g.N = 3 * n; g.K = n;
+      g.xf32 = x_d; g.ln_g = e.ln1_g; g.ln_b = e.ln1_b; g.ln_eps = 1e-5f;
+      g.out = q_d; g.ldo = n; g.hs_state = n; g.hs_heads = nh;
+      g.row_win = rw; g.row_slot = rs; g.row_pos = rp; g.kc = kc[l]; g.vc = vc[l]; g.kv_beams = Gcap; g.kv_ctx = CTX;
+      TRY(p1(g, EPI_QKV_DEC, true));
+      launch_self_attn<T>(q_d, n, kc[l], vc[l], rw, rs, rp, S.anc, ancG, Gcap, nh, CTX, att_d, n, R, st);
+      g = GemmArgs();
+      g.X = att_d; g.ldx = n; g.W = e.wo; g.bias = e.bo; g.M = R; g.N = n; g.K = n; g.out_f32 = x_d; g.ldo = n;
+      TRY(p1(g, EPI_RESID, false));
+      // cross-attention block
+      g = GemmArgs();
+      g.W = e.wqx; g.bias = e.bqx; g.M = R; g.N = n; g.K = n;
+      g.xf32 = x_d; g.ln_g = e.lnx_g; g.ln_b = e.lnx_b; g.ln_eps = 1e-5f; g.out = q_d; g.ldo = n;
+      TRY(p1(g, EPI_STORE, true));
+      XQPart xq;
+      xq.max_rows = ancG;
+      const T* ck = ckv + (size_t)(2 * l) * Wcap * TKP * n;
+      const T* cv = ckv + (size_t)(2 * l + 1) * Wcap * TKP * n;
+      launch_cross_attn<T>(q_d, n, ck, cv, 1500, nh, NSPLIT, nwin, wr0, wnr, wsl, (int64_t)TKP * n, po, pm, pl, att_d,
+                           n, R, nullptr, nullptr, 0, st, xq);
+      g = GemmArgs();
+      g.X = att_d; g.ldx = n; g.W = e.wox; g.bias = e.box; g.M = R; g.N = n; g.K = n; g.out_f32 = x_d; g.ldo = n;
+      TRY(p1(g, EPI_RESID, false));
+      // MLP
+      g = GemmArgs();
+      g.W = e.w1; g.bias = e.b1; g.M = R; g.N = 4 * n; g.K = n;
+      g.xf32 = x_d; g.ln_g = e.ln2_g; g.ln_b = e.ln2_b; g.ln_eps = 1e-5f; g.out = hm_d; g.ldo = 4 * n;
+      TRY(p1(g, EPI_STORE_GELU, true));
+      g = GemmArgs();
+      g.X = hm_d; g.ldx = 4 * n; g.W = e.w2; g.bias = e.b2; g.M = R; g.N = n; g.K = 4 * n; g.out_f32 = x_d; g.ldo = n;
+      TRY(p1(g, EPI_RESID, false));
+    }
+    launch_layernorm<T>(x_d, xn_d, ln_g, ln_b, R, n, 1e-5f, nullptr, st);
     return 0;
   }
 
@@ -1418,14 +1537,8 @@ struct Ctx : public wh_ctx {
         for (int l = 0; l < nl; ++l) {
           auto& e = dec[l];
           if (what == 2) {
-            struct P { const T* X; int K; const T* W; int N; } ps[6] = {
-                {xn_d, n, e.wqkv, 3 * n}, {att_d, n, e.wo, n}, {xn_d, n, e.wqx, n},
-                {att_d, n, e.wox, n},     {xn_d, n, e.w1, 4 * n}, {hm_d, 4 * n, e.w2, n}};
-            for (auto& p : ps) {
-              int ks = 0;
-              TRY(partial(p.X, p.K, p.W, R, p.N, p.K, &ks));
-              ++launches;
-            }
+            TRY(layer_projections(l, R));
+            launches += 6;
           } else {
             const T* ck = ckv + (size_t)(2 * l) * Wcap * TKP * n;
             const T* cv = ckv + (size_t)(2 * l + 1) * Wcap * TKP * n;
