@@ -35,7 +35,25 @@ struct XQPart {
   int z = 0;
   const float* bias = nullptr;
   int max_rows = 0;  // rows per window when known (decoder step: the beam group)
+  // k_cross_attn1 key split (few windows): per-split records [win][head][split][XREC]
+  // and one arrival counter per (window, head), zero between launches; null = no split
+  float* split_rec = nullptr;
+  int* split_cnt = nullptr;
 };
+constexpr int XREC = 16 * 64 + 32;  // floats per split record: O[16][64], m[16], l[16]
+constexpr int XSPLIT_MAX = 8;
+// key splits per (window, head) for the step cross-attention: spread the keys of few
+// windows over ~256 workgroups (1 window: 20 workgroups would leave 236 CUs idle);
+// WHISPER_HIP_XSPLIT caps it (A/B; 1 = no split)
+int cross_attn_split_cap();
+inline int cross_attn_splits(int nwin, int H) {
+  const int pairs = nwin * H;
+  if (pairs >= 128) return 1;
+  int s = 256 / pairs;
+  const int cap = cross_attn_split_cap();
+  if (s > cap) s = cap;
+  return s < 1 ? 1 : s > XSPLIT_MAX ? XSPLIT_MAX : s;
+}
 inline bool cross_attn_q_slabs(int z) { return z == 4 || z == 8 || z == 10; }
 template <typename T>
 void launch_cross_attn(const T* q, int ldq, const T* ck, const T* cv, int Tk, int H, int nsplit, int nwin,

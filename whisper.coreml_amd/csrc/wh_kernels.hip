@@ -772,12 +772,18 @@ __global__ __launch_bounds__(64) void k_cross_combine(const float* __restrict__ 
   out[(int64_t)row * ldo + h * 64 + lane] = from_f32<T>(num / den);
 }
 
-// Decoder-step variant: ONE workgroup per (window, head) covers all keys, so there is
-// no split partial and no k_cross_combine launch.  8 waves; wave w takes tiles
-// w, w+8, w+16, ... (TPW per wave, compile-time) with an online softmax, the next
-// tile's K/V fragments in flight while the current tile is computed; the 8 waves'
-// (m, l, O) are merged in LDS and the normalised rows written as T.  <= 16 rows per
-// window (beams of a step), query from q or reduced from split-K slabs (QZ > 0).
+// Decoder-step variant: one workgroup per (window, head, key split); without a split
+// (gridDim.z == 1, many windows) it covers all keys, so there is no partial and no
+// k_cross_combine launch.  8 waves; wave w takes the split's tiles w, w+8, ... (split s
+// of S owns the tiles t = s + S*j) with an online softmax, the next tile's K/V fragments
+// in flight while the current tile is computed; the 8 waves' (m, l, O) are merged in
+// LDS.  S == 1: the normalised rows are written as T.  S > 1 (few windows: the keys of
+// one window's 20 heads spread over ~160 workgroups instead of 20): each split writes
+// its (O, m, l) record write-through (sc1), drains it and adds to the (window, head)
+// counter (relaxed agent atomic); the workgroup drawing S-1 re-arms the counter and
+// combines the S records in split order (sc1 loads; deterministic for any arrival
+// order; cdna_hip_programming.md §6 Guideline 16 R1).  <= 16 rows per window (beams of
+// a step), query from q or reduced from split-K slabs (QZ > 0).
 template <typename T, int QZ, int TPW, int PF>
 __global__ __launch_bounds__(512, PF ? 1 : 2) void k_cross_attn1(const T* __restrict__ q, int ldq, const T* ck, const T* cvt,
                                                      int Tk, const int* __restrict__ win_row0,
@@ -789,7 +795,8 @@ __global__ __launch_bounds__(512, PF ? 1 : 2) void k_cross_attn1(const T* __rest
   __shared__ float red_m[NW][16], red_l[NW][16];
   __shared__ float red_o[NW][64][17];
   __shared__ __attribute__((aligned(16))) T qs[32][72];
-  const int wi = blockIdx.x, h = blockIdx.y, H = gridDim.y;
+  __shared__ int s_ticket;
+  const int wi = blockIdx.x, h = blockIdx.y, H = gridDim.y, S = gridDim.z, sp = blockIdx.z;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int r = lane & 15, g = lane >> 4;
   const int row0 = win_row0[wi], nrows = win_nrows[wi];
@@ -799,7 +806,7 @@ __global__ __launch_bounds__(512, PF ? 1 : 2) void k_cross_attn1(const T* __rest
   // loads are never branched around (a branch turns the compiler's counted waits into
   // full drains): tiles past the end reload the wave's first tile and skip the math
   auto load_kv = [&](int it, Frag<T> (&kf)[4][2], Frag<T> (&vf)[4][2]) {
-    const int t = wave + NW * it, kt0 = (t < ntiles ? t : wave) * 64;
+    const int t = sp + S * (wave + NW * it), kt0 = (t < ntiles ? t : sp) * 64;
 #pragma unroll
     for (int kt = 0; kt < 4; ++kt) {
       const T* kp = kbase + (int64_t)(kt0 + kt * 16 + r) * 64 + 8 * g;
@@ -858,7 +865,7 @@ __global__ __launch_bounds__(512, PF ? 1 : 2) void k_cross_attn1(const T* __rest
     } else if constexpr (PF == 0) {
       if (it > 0) load_kv(it, kf[0], vf[0]);
     }
-    const int t = wave + NW * it;
+    const int t = sp + S * (wave + NW * it);
     if (t < ntiles) {
       const int kt0 = t * 64;
       float4_t sc[4];
@@ -912,9 +919,9 @@ __global__ __launch_bounds__(512, PF ? 1 : 2) void k_cross_attn1(const T* __rest
 #pragma unroll
     for (int j = 0; j < 4; ++j) red_o[wave][dt * 16 + 4 * g + j][r] = acc[dt][j];
   __syncthreads();
-  if (tid < 256) {
-    const int qq = tid >> 4, dc = (tid & 15) * 4;
-    if (qq < nrows) {
+  const int qq = tid >> 4, dc = (tid & 15) * 4;
+  if (S == 1) {
+    if (tid < 256 && qq < nrows) {
       float M = -INFINITY;
 #pragma unroll
       for (int w = 0; w < NW; ++w) M = fmaxf(M, red_m[w][qq]);
@@ -935,7 +942,73 @@ __global__ __launch_bounds__(512, PF ? 1 : 2) void k_cross_attn1(const T* __rest
       }
       store4(out + (int64_t)(row0 + qq) * ldo + h * 64 + dc, o[0], o[1], o[2], o[3]);
     }
+    return;
   }
+  // split: this split's (O unnormalised, m, l) record, write-through
+  typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+  const auto rs = __builtin_amdgcn_make_buffer_rsrc(xq.split_rec, 0, 0x7fffffff, 0x00020000);
+  const int pair = wi * H + h;
+  if (tid < 256) {
+    float M = -INFINITY;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) M = fmaxf(M, red_m[w][qq]);
+    float f[NW], L = 0.f;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) {
+      f[w] = red_m[w][qq] == -INFINITY ? 0.f : exp2f((red_m[w][qq] - M) * LOG2E);
+      L += f[w] * red_l[w][qq];
+    }
+    float4_t o = (float4_t){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+#pragma unroll
+      for (int w = 0; w < NW; ++w) o[e] += f[w] * red_o[w][dc + e][qq];
+    const int rb = (pair * S + sp) * XREC * 4;  // record byte offset
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, o), rs, rb + (qq * 64 + dc) * 4, 0, 16);
+    if (dc == 0) {
+      __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, M), rs, rb + (1024 + qq) * 4, 0, 16);
+      __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, L), rs, rb + (1040 + qq) * 4, 0, 16);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its stores
+  }
+  __syncthreads();
+  if (tid == 0) s_ticket = __hip_atomic_fetch_add(xq.split_cnt + pair, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __syncthreads();
+  if (s_ticket != S - 1) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // no instruction: keeps the loads below the add
+  if (tid == 0) __hip_atomic_store(xq.split_cnt + pair, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (tid >= 256 || qq >= nrows) return;
+  float4_t ov[XSPLIT_MAX];
+  float mv[XSPLIT_MAX], lv[XSPLIT_MAX];
+#pragma unroll
+  for (int s = 0; s < XSPLIT_MAX; ++s) {  // every record load issued first (clamped index)
+    const int rb = (pair * S + min(s, S - 1)) * XREC * 4;
+    ov[s] = __builtin_bit_cast(float4_t, __builtin_amdgcn_raw_buffer_load_b128(rs, rb + (qq * 64 + dc) * 4, 0, 16));
+    mv[s] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, rb + (1024 + qq) * 4, 0, 16));
+    lv[s] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, rb + (1040 + qq) * 4, 0, 16));
+  }
+  float M = -INFINITY;
+#pragma unroll
+  for (int s = 0; s < XSPLIT_MAX; ++s)
+    if (s < S) M = fmaxf(M, mv[s]);
+  float L = 0.f;
+  float4_t o = (float4_t){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int s = 0; s < XSPLIT_MAX; ++s) {
+    const float f = (s < S && mv[s] != -INFINITY) ? exp2f((mv[s] - M) * LOG2E) : 0.f;
+    L += f * lv[s];
+    o += f * ov[s];
+  }
+  const float inv = 1.f / L;
+  store4(out + (int64_t)(row0 + qq) * ldo + h * 64 + dc, o[0] * inv, o[1] * inv, o[2] * inv, o[3] * inv);
+}
+
+int cross_attn_split_cap() {
+  static const int cap = [] {
+    const char* e = getenv("WHISPER_HIP_XSPLIT");
+    return e ? atoi(e) : XSPLIT_MAX;
+  }();
+  return cap;
 }
 
 template <typename T>
@@ -952,9 +1025,11 @@ void launch_cross_attn(const T* q, int ldq, const T* ck, const T* cv, int Tk, in
     const char* e = getenv("WHISPER_HIP_XATTN1_PF");
     return e ? atoi(e) : 1;
   }();
-  const int ntiles = (Tk + 63) / 64, tpw = (ntiles + 7) / 8;
+  const int ntiles = (Tk + 63) / 64;
+  const int nsp = xq.split_rec && xq.split_cnt ? cross_attn_splits(nwin, H) : 1;
+  const int tpw = ((ntiles + nsp - 1) / nsp + 7) / 8;
   if (one && xq.max_rows >= 1 && xq.max_rows <= 16 && !qk_map && tpw <= 4) {
-    const dim3 g1(nwin, H);
+    const dim3 g1(nwin, H, nsp);
 #define XA1(QZ_, TPW_)                                                                                       \
   if (pf == 2) k_cross_attn1<T, QZ_, TPW_, 2><<<g1, 512, 0, st>>>(q, ldq, ck, cv, Tk, win_row0, win_nrows, win_slot, \
                                                                   win_stride, xq, out, ldo);                       \

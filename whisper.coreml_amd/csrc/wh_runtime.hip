@@ -186,6 +186,17 @@ struct Ctx : public wh_ctx {
   static constexpr int P1_SLABS = 2048;  // k_proj1 split-K slabs: zs x 16-column tiles <= 16 x 80 at n = 1280
   float* p1_slab = nullptr;  // k_proj1 in-launch split-K slabs [zs][N/16][256]
   int* p1_cnt = nullptr;     // and arrival counters [4n/16] (zero between launches)
+  float* xs_rec = nullptr;   // step cross-attention key-split records (<= 256 x XREC)
+  int* xs_cnt = nullptr;     // and (window, head) arrival counters (< 128 pairs split)
+
+  // the step cross-attention's query / split arguments
+  XQPart step_xq(int rows_per_window) const {
+    XQPart xq;
+    xq.max_rows = rows_per_window;
+    xq.split_rec = xs_rec;
+    xq.split_cnt = xs_cnt;
+    return xq;
+  }
   int* qk_map;  // [Ld][nh]
   unsigned* suppress;
   DecState S;
@@ -318,6 +329,7 @@ struct Ctx : public wh_ctx {
     addA(64);
     addA(64);
     addA((size_t)P1_SLABS * 256 * 4); addA((size_t)(4 * n / 16) * 4);  // k_proj1 split-K slabs + counters
+    addA((size_t)256 * XREC * 4); addA(128 * 4);                             // cross-attention split records
     HIPCHK(hipMalloc(&abase, ab));
     HIPCHK(hipMemset(abase, 0, ab));
     aa.base = (char*)abase;
@@ -351,7 +363,8 @@ struct Ctx : public wh_ctx {
     S.lpart = fa((size_t)Wcap * Gcap * LP_SLICES * LP_REC);
     S.seed = (unsigned long long*)aa.take(64);
     p1_slab = fa((size_t)P1_SLABS * 256); p1_cnt = ia(4 * n / 16);  // zeroed with the arena
-    if (!S.seed || !S.cand_idx || !p1_cnt) return fail(-3, "activation arena overflow");
+    xs_rec = fa((size_t)256 * XREC); xs_cnt = ia(128);
+    if (!S.seed || !S.cand_idx || !p1_cnt || !xs_cnt) return fail(-3, "activation arena overflow");
     S.nw = Wcap; S.G = 1; S.ctx = CTX; S.hctx = HCTX; S.maxc = 16;
     HIPCHK(hipMalloc(&d_gmax, 64));
     d_gmax_f = (float*)(d_gmax + 4);
@@ -778,7 +791,7 @@ struct Ctx : public wh_ctx {
       // cross-attention query: in step mode its split-K slabs are reduced inside
       // k_cross_attn (rows per window <= Gcap <= 8), otherwise projected directly
       XQPart xq;
-      if (skinny) xq.max_rows = ancG;
+      if (skinny) xq = step_xq(ancG);
       if (skinny && xq_fused) {
         int ks = 0;
         TRY(partial(xn_d, n, e.wqx, R, n, n, &ks));
@@ -892,8 +905,7 @@ struct Ctx : public wh_ctx {
       g.W = e.wqx; g.bias = e.bqx; g.M = R; g.N = n; g.K = n;
       g.xf32 = x_d; g.ln_g = e.lnx_g; g.ln_b = e.lnx_b; g.ln_eps = 1e-5f; g.out = q_d; g.ldo = n;
       TRY(p1(g, EPI_STORE, true));
-      XQPart xq;
-      xq.max_rows = ancG;
+      const XQPart xq = step_xq(ancG);
       const T* ck = ckv + (size_t)(2 * l) * Wcap * TKP * n;
       const T* cv = ckv + (size_t)(2 * l + 1) * Wcap * TKP * n;
       launch_cross_attn<T>(q_d, n, ck, cv, 1500, nh, NSPLIT, nwin, wr0, wnr, wsl, (int64_t)TKP * n, po, pm, pl, att_d,
@@ -1542,8 +1554,7 @@ struct Ctx : public wh_ctx {
           } else {
             const T* ck = ckv + (size_t)(2 * l) * Wcap * TKP * n;
             const T* cv = ckv + (size_t)(2 * l + 1) * Wcap * TKP * n;
-            XQPart xq;  // the step's kernel (k_cross_attn1), query from q_d
-            xq.max_rows = cur_G;
+            const XQPart xq = step_xq(cur_G);  // the step's kernel (k_cross_attn1), query from q_d
             launch_cross_attn<T>(q_d, n, ck, cv, 1500, nh, NSPLIT, cur_nwin, st_win_row0, st_win_nrows, st_win_slot,
                                  (int64_t)TKP * n, po, pm, pl, att_d, n, R, nullptr, nullptr, 0, st, xq);
             ++launches;
