@@ -1,8 +1,9 @@
 """HBM traffic per launch of the decoder-step kernels from rocprofv3 PMC counters.
 
 Workload (`run`): large-v3 fp16 at the bench batch (20 windows x beam 5 = 100 rows),
-encode + decode_begin, then wh_time_stage 2 (the six split-K projections (k_proj) of every
-decoder layer) and 3 (cross-attention of every layer) once each.
+encode (k_gemm_256) + decode_begin, then wh_time_stage 2 (the six split-K projections
+(k_proj) of every decoder layer) and 3 (cross-attention of every layer) once each; then
+one window (5 rows) and stage 2 again (the k_proj1 projections).
 
 Collected in two separate passes (FETCH_SIZE and WRITE_SIZE do not fit one TCC pass
 on gfx950, MI355X_MICROARCH.md "rocprofv3 PMC slots"):
@@ -12,7 +13,7 @@ on gfx950, MI355X_MICROARCH.md "rocprofv3 PMC slots"):
       python $R/profiles/pmc_traffic.py run
   rocprofv3 --pmc WRITE_SIZE --kernel-trace -d $R/gpurun_out/pmc_w -o run --output-format csv -- \
       python $R/profiles/pmc_traffic.py run
-  python profiles/pmc_traffic.py parse gpurun_out/pmc_f gpurun_out/pmc_w > profiles/r01/traffic.json
+  python profiles/pmc_traffic.py parse gpurun_out/pmc_f gpurun_out/pmc_w > profiles/r02/traffic.json
 
 Correction (same guide, "HBM [CDNA4]"): FETCH_SIZE counts half the bytes of 16 B/lane
 streaming reads on gfx950, so reads = 2 x FETCH_SIZE; WRITE_SIZE is exact for 16 B
@@ -30,8 +31,10 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 KERNELS = {
     # short name -> regex on the mangled kernel name
-    "k_proj": r"k_projIDF16_",                # fp16 split-K projections (all tile variants)
-    "k_cross_attn1": r"k_cross_attn1IDF16_",      # the step's single-split cross-attention
+    "k_proj": r"k_projIDF16_",                # fp16 split-K projections (all tile variants), 100 rows
+    "k_proj1": r"k_proj1IDF16_",              # single-window projections (5 rows, all six shapes)
+    "k_cross_attn1": r"k_cross_attn1IDF16_",  # the step's cross-attention, 20 windows (no key split)
+    "k_gemm_256": r"k_gemm_256",              # encoder GEMMs of the 20-window encode (all epilogues)
 }
 
 
@@ -51,6 +54,9 @@ def run():
     model.ctx.decode_begin(task.wh_opts(), [task.initial_tokens] * 20, [task.sot_index] * 20)
     print("gemv ms/launch", model.ctx.time_stage(2, 1))
     print("cross-attn ms/launch", model.ctx.time_stage(3, 1))
+    # one window (5 rows): the six projections of every layer as k_proj1 launches
+    model.ctx.decode_begin(task.wh_opts(), [task.initial_tokens], [task.sot_index])
+    print("k_proj1 ms/launch", model.ctx.time_stage(2, 1))
     model.close()
 
 
