@@ -45,14 +45,16 @@ constexpr int XSPLIT_MAX = 8;
 // key splits per (window, head) for the step cross-attention: spread the keys of few
 // windows over ~256 workgroups (1 window: 20 workgroups would leave 236 CUs idle);
 // WHISPER_HIP_XSPLIT caps it (A/B; 1 = no split)
+constexpr int XREC_CAP = 2048;  // split records allocated per context
 int cross_attn_split_cap();
+int cross_attn_split_big();
 inline int cross_attn_splits(int nwin, int H) {
   const int pairs = nwin * H;
-  if (pairs >= 128) return 1;
-  int s = 256 / pairs;
+  int s = pairs >= 128 ? cross_attn_split_big() : 256 / pairs;
   const int cap = cross_attn_split_cap();
   if (s > cap) s = cap;
-  return s < 1 ? 1 : s > XSPLIT_MAX ? XSPLIT_MAX : s;
+  s = s < 1 ? 1 : s > XSPLIT_MAX ? XSPLIT_MAX : s;
+  return pairs * s <= XREC_CAP ? s : 1;
 }
 inline bool cross_attn_q_slabs(int z) { return z == 4 || z == 8 || z == 10; }
 template <typename T>

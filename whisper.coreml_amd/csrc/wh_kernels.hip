@@ -1003,6 +1003,14 @@ __global__ __launch_bounds__(512, PF ? 1 : 2) void k_cross_attn1(const T* __rest
   store4(out + (int64_t)(row0 + qq) * ldo + h * 64 + dc, o[0] * inv, o[1] * inv, o[2] * inv, o[3] * inv);
 }
 
+int cross_attn_split_big() {  // splits at >= 128 (window, head) pairs (WHISPER_HIP_XSPLIT_BIG, A/B)
+  static const int v = [] {
+    const char* e = getenv("WHISPER_HIP_XSPLIT_BIG");
+    return e ? atoi(e) : 1;
+  }();
+  return v;
+}
+
 int cross_attn_split_cap() {
   static const int cap = [] {
     const char* e = getenv("WHISPER_HIP_XSPLIT");

@@ -186,8 +186,8 @@ struct Ctx : public wh_ctx {
   static constexpr int P1_SLABS = 2048;  // k_proj1 split-K slabs: zs x 16-column tiles <= 16 x 80 at n = 1280
   float* p1_slab = nullptr;  // k_proj1 in-launch split-K slabs [zs][N/16][256]
   int* p1_cnt = nullptr;     // and arrival counters [4n/16] (zero between launches)
-  float* xs_rec = nullptr;   // step cross-attention key-split records (<= 256 x XREC)
-  int* xs_cnt = nullptr;     // and (window, head) arrival counters (< 128 pairs split)
+  float* xs_rec = nullptr;   // step cross-attention key-split records (<= XREC_CAP x XREC)
+  int* xs_cnt = nullptr;     // and (window, head) arrival counters
 
   // the step cross-attention's query / split arguments
   XQPart step_xq(int rows_per_window) const {
@@ -329,7 +329,7 @@ struct Ctx : public wh_ctx {
     addA(64);
     addA(64);
     addA((size_t)P1_SLABS * 256 * 4); addA((size_t)(4 * n / 16) * 4);  // k_proj1 split-K slabs + counters
-    addA((size_t)256 * XREC * 4); addA(128 * 4);                             // cross-attention split records
+    addA((size_t)XREC_CAP * XREC * 4); addA((size_t)Wcap * nh * 4);           // cross-attention split records
     HIPCHK(hipMalloc(&abase, ab));
     HIPCHK(hipMemset(abase, 0, ab));
     aa.base = (char*)abase;
@@ -363,7 +363,7 @@ struct Ctx : public wh_ctx {
     S.lpart = fa((size_t)Wcap * Gcap * LP_SLICES * LP_REC);
     S.seed = (unsigned long long*)aa.take(64);
     p1_slab = fa((size_t)P1_SLABS * 256); p1_cnt = ia(4 * n / 16);  // zeroed with the arena
-    xs_rec = fa((size_t)256 * XREC); xs_cnt = ia(128);
+    xs_rec = fa((size_t)XREC_CAP * XREC); xs_cnt = ia((size_t)Wcap * nh);
     if (!S.seed || !S.cand_idx || !p1_cnt || !xs_cnt) return fail(-3, "activation arena overflow");
     S.nw = Wcap; S.G = 1; S.ctx = CTX; S.hctx = HCTX; S.maxc = 16;
     HIPCHK(hipMalloc(&d_gmax, 64));
