@@ -122,8 +122,8 @@ WH_DEV void epilogue_store(const GemmArgs& a, int m, int gi, int ri, int n, floa
 template <typename T>
 int launch_gemm(const GemmArgs& a, int epi, hipStream_t st);
 // launch_gemm with the large-M tile chosen explicitly: 256 = k_gemm_256 where the shape
-// allows it, 128 = k_gemm_tile (tools/gemm_bench A/B; launch_gemm uses 256 unless
-// WHISPER_HIP_GEMM=128)
+// allows it, 128 = k_gemm_tile (128 x 64 tiles below 256 tiles), 129 = k_gemm_tile with
+// 128 x 128 tiles only (tools/gemm_bench A/B; launch_gemm uses 256 unless WHISPER_HIP_GEMM)
 template <typename T>
 int launch_gemm_tiles(const GemmArgs& a, int epi, int tile_sel, hipStream_t st);
 

@@ -26,17 +26,21 @@ namespace wh {
 constexpr int TBM = 128, TBN = 128, TKB = 128;  // TKB = bytes of K per tile row
 constexpr int TROW = TKB + 16;                  // padded LDS row stride (bytes): conflict-free b128 reads
 
-template <typename T, int EPI>
+// TBN_ = 128 or 64 output columns per tile (64: grids below one tile per CU, e.g. the
+// n-wide encoder GEMMs of a single window: 120 -> 240 workgroups)
+template <typename T, int EPI, int TBN_ = TBN>
 __global__ __launch_bounds__(256, 2) void k_gemm_tile(GemmArgs a) {
   constexpr int BK = TKB / (int)sizeof(T);  // 64 half / 32 float
   constexpr int KS = BK / 32;               // k-steps per tile
-  __shared__ __attribute__((aligned(16))) char smem[2][2][TBM * TROW];  // [buf][A/W][rows*stride]
+  constexpr int WCH = TBN_ / 32;            // W chunks per thread (TBN_ rows x 8 chunks / 256)
+  constexpr int NI = TBN_ / 32;             // 16-column fragments per wave (wave tile 64 x TBN_/2)
+  __shared__ __attribute__((aligned(16))) char smem[2][(TBM + TBN_) * TROW];  // [buf][X rows | W rows]
 
-  const int ntn = a.N / TBN;
+  const int ntn = a.N / TBN_;
   const int ntm = (a.M + TBM - 1) / TBM;
   const int bid = xcd_remap(blockIdx.x, ntm * ntn);
   const int tm = bid / ntn, tn = bid % ntn;
-  const int m0 = tm * TBM, n0 = tn * TBN;
+  const int m0 = tm * TBM, n0 = tn * TBN_;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wr = wave >> 1, wc = wave & 1;
   const int r = lane & 15, g = lane >> 4;
@@ -44,9 +48,9 @@ __global__ __launch_bounds__(256, 2) void k_gemm_tile(GemmArgs a) {
   const T* X = reinterpret_cast<const T*>(a.X);
   const T* W = reinterpret_cast<const T*>(a.W);
 
-  // per-thread global source rows for the 4 chunks of each operand (16 B chunks, 8 per row)
+  // per-thread global source rows of its 16 B chunks (8 per row): 4 of X, WCH of W
   const char* xsrc[4];
-  const char* wsrc[4];
+  const char* wsrc[WCH];
   int lds_off[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
@@ -56,7 +60,7 @@ __global__ __launch_bounds__(256, 2) void k_gemm_tile(GemmArgs a) {
     if (m >= a.M) m = a.M - 1;
     const int gi = m / a.x_group_rows, ri = m - gi * a.x_group_rows;
     xsrc[i] = reinterpret_cast<const char*>(X + (int64_t)gi * a.x_group_stride + (int64_t)ri * a.ldx) + col * 16;
-    wsrc[i] = reinterpret_cast<const char*>(W + (int64_t)(n0 + row) * a.K) + col * 16;
+    if (i < WCH) wsrc[i] = reinterpret_cast<const char*>(W + (int64_t)(n0 + row) * a.K) + col * 16;
     lds_off[i] = row * TROW + col * 16;
   }
   // two register sets: the global loads of tile kt+2 are in flight while tile kt is
@@ -64,47 +68,45 @@ __global__ __launch_bounds__(256, 2) void k_gemm_tile(GemmArgs a) {
   // load has a whole k-step of MFMAs to land.  Loads are unconditional (the tail
   // re-reads the last tile) so the compiler's waits stay counted, and the barrier
   // waits for LDS only — __syncthreads() would drain the tile in flight.
-  float4_t ra[8], rb[8];  // [0..3] X chunks, [4..7] W chunks
+  float4_t ra[4 + WCH], rb[4 + WCH];  // [0..3] X chunks, [4..] W chunks
   auto gload = [&](int kt, float4_t* rg) {
     const int kb = kt * TKB;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      rg[i] = *reinterpret_cast<const float4_t*>(xsrc[i] + kb);
-      rg[4 + i] = *reinterpret_cast<const float4_t*>(wsrc[i] + kb);
-    }
+    for (int i = 0; i < 4; ++i) rg[i] = *reinterpret_cast<const float4_t*>(xsrc[i] + kb);
+#pragma unroll
+    for (int i = 0; i < WCH; ++i) rg[4 + i] = *reinterpret_cast<const float4_t*>(wsrc[i] + kb);
   };
   auto sstore = [&](int buf, const float4_t* rg) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      *reinterpret_cast<float4_t*>(&smem[buf][0][lds_off[i]]) = rg[i];
-      *reinterpret_cast<float4_t*>(&smem[buf][1][lds_off[i]]) = rg[4 + i];
-    }
+    for (int i = 0; i < 4; ++i) *reinterpret_cast<float4_t*>(&smem[buf][lds_off[i]]) = rg[i];
+#pragma unroll
+    for (int i = 0; i < WCH; ++i) *reinterpret_cast<float4_t*>(&smem[buf][TBM * TROW + lds_off[i]]) = rg[4 + i];
   };
   auto lds_barrier = [] { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); };
 
-  float4_t acc[4][4];
+  float4_t acc[4][NI];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = (float4_t){0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < NI; ++j) acc[i][j] = (float4_t){0.f, 0.f, 0.f, 0.f};
 
   auto compute = [&](int buf) {
-    const char* As = smem[buf][0];
-    const char* Ws = smem[buf][1];
+    const char* As = smem[buf];
+    const char* Ws = smem[buf] + TBM * TROW;
 #pragma unroll
     for (int s = 0; s < KS; ++s) {
       const int koff = (32 * s + 8 * g) * (int)sizeof(T);
-      Frag<T> wf[4], xf[4];
+      Frag<T> wf[NI], xf[4];
 #pragma unroll
-      for (int ni = 0; ni < 4; ++ni)
-        frag_load(wf[ni], reinterpret_cast<const T*>(Ws + (wc * 64 + ni * 16 + r) * TROW + koff));
+      for (int ni = 0; ni < NI; ++ni)
+        frag_load(wf[ni], reinterpret_cast<const T*>(Ws + (wc * (TBN_ / 2) + ni * 16 + r) * TROW + koff));
 #pragma unroll
       for (int mi = 0; mi < 4; ++mi)
         frag_load(xf[mi], reinterpret_cast<const T*>(As + (wr * 64 + mi * 16 + r) * TROW + koff));
 #pragma unroll
       for (int mi = 0; mi < 4; ++mi)
 #pragma unroll
-        for (int ni = 0; ni < 4; ++ni) mfma_step(acc[mi][ni], wf[ni], xf[mi]);
+        for (int ni = 0; ni < NI; ++ni) mfma_step(acc[mi][ni], wf[ni], xf[mi]);
     }
   };
 
@@ -127,15 +129,15 @@ __global__ __launch_bounds__(256, 2) void k_gemm_tile(GemmArgs a) {
     lds_barrier();
   }
 
-  // epilogue: lane holds Y[m = m0+wr*64+mi*16+r][n = n0+wc*64+ni*16+4g .. +3]
+  // epilogue: lane holds Y[m = m0+wr*64+mi*16+r][n = n0+wc*TBN_/2+ni*16+4g .. +3]
 #pragma unroll
   for (int mi = 0; mi < 4; ++mi) {
     const int m = m0 + wr * 64 + mi * 16 + r;
     if (m >= a.M) continue;
     const int gi = m / a.x_group_rows, ri = m - gi * a.x_group_rows;
 #pragma unroll
-    for (int ni = 0; ni < 4; ++ni) {
-      const int n = n0 + wc * 64 + ni * 16 + 4 * g;
+    for (int ni = 0; ni < NI; ++ni) {
+      const int n = n0 + wc * (TBN_ / 2) + ni * 16 + 4 * g;
       float4_t v = acc[mi][ni];
       if (a.bias) {
         const float4_t b = load4f(a.bias + n);
@@ -585,9 +587,17 @@ int launch_gemm_tiles(const GemmArgs& a, int epi, int tile_sel, hipStream_t st) 
       default: return -1;
     }
   } else if (big) {
-    const int nwg = ((a.M + TBM - 1) / TBM) * (a.N / TBN);
+    const int ntm = (a.M + TBM - 1) / TBM;
+    // under one 128 x 128 tile per CU, 128 x 64 tiles double the grid (a single window's
+    // n-wide encoder GEMMs: 120 -> 240 workgroups)
+    const bool half = ntm * (a.N / TBN) < 256 && (a.N % 64) == 0 && tile_sel != 129;
+    const int nwg = ntm * (a.N / (half ? 64 : TBN));
     switch (epi) {
-#define CASE(E) case E: k_gemm_tile<T, E><<<nwg, 256, 0, st>>>(a); break;
+#define CASE(E)                                                       \
+  case E:                                                             \
+    if (half) k_gemm_tile<T, E, 64><<<nwg, 256, 0, st>>>(a);          \
+    else k_gemm_tile<T, E><<<nwg, 256, 0, st>>>(a);                   \
+    break;
       CASE(EPI_STORE) CASE(EPI_STORE_GELU) CASE(EPI_RESID) CASE(EPI_GELU_POS) CASE(EPI_HEADSPLIT) CASE(EPI_QKV_DEC)
       CASE(EPI_QKV_ENC)
 #undef CASE

@@ -1,5 +1,6 @@
-// Encoder GEMM check + A/B: k_gemm_256 (launch_gemm_tiles(..., 256)) against
-// k_gemm_tile (..., 128) on the large-v3 encoder shapes, uniform random [-1, 1) fp16
+// Encoder GEMM check + A/B: the launcher's choice (launch_gemm_tiles(..., 256): k_gemm_256
+// from 256 tiles, else k_gemm_tile with 128 x 64 tiles below 256 tiles) against
+// k_gemm_tile with 128 x 128 tiles (..., 129) on the large-v3 encoder shapes, uniform random [-1, 1) fp16
 // operands (cdna_hip_programming.md §5.4 rule 25: never zero-filled).
 //   * correctness: every output of both kernels against each other (max |diff| relative to
 //     the output scale) and 4096 sampled outputs against an fp64 host dot product;
@@ -51,6 +52,7 @@ int main(int argc, char** argv) {
       {"qkv", M, 3840, 1280, 1500, 0}, {"out", M, 1280, 1280, 1500, 0}, {"fc1", M, 5120, 1280, 1500, 0},
       {"fc2", M, 1280, 5120, 1500, 0}, {"grouped", M, 1280, 1280, 1500, 2},
       {"ragged", 1000 + 37, 1280, 1280, 1 << 30, 0}, {"one-window", 1500, 5120, 1280, 1500, 0},
+      {"1w-out", 1500, 1280, 1280, 1500, 0}, {"1w-fc2", 1500, 1280, 5120, 1500, 0},
   };
   std::mt19937 rng(1234);
   std::uniform_real_distribution<float> uni(-1.f, 1.f);
@@ -91,7 +93,7 @@ int main(int argc, char** argv) {
     a1.out = Y1;
     CK(hipMemset(Y0, 0, (size_t)s.M * s.N * 2));
     CK(hipMemset(Y1, 0, (size_t)s.M * s.N * 2));
-    if (launch_gemm_tiles<half_t>(a0, EPI_STORE, 128, 0) || launch_gemm_tiles<half_t>(a1, EPI_STORE, 256, 0)) {
+    if (launch_gemm_tiles<half_t>(a0, EPI_STORE, 129, 0) || launch_gemm_tiles<half_t>(a1, EPI_STORE, 256, 0)) {
       printf("%s: launch refused\n", s.name);
       return 1;
     }
@@ -121,7 +123,7 @@ int main(int argc, char** argv) {
     std::vector<float> t128, t256;
     for (int rd = 0; rd < rounds; ++rd) {
       for (int v = 0; v < 2; ++v) {
-        const int tile = v ? 256 : 128;
+        const int tile = v ? 256 : 129;
         GemmArgs& av = v ? a1 : a0;
         launch_gemm_tiles<half_t>(av, EPI_STORE, tile, 0);
         CK(hipEventRecord(e0, 0));
