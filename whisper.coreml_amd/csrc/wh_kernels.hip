@@ -153,8 +153,9 @@ void launch_resid_ln(float* x, const float* part, int nsplit, int64_t part_strid
 // LDS feeds ENC_RT MFMAs.  S^T = K Q^T and O^T = V^T P^T so each lane owns one query row per row tile
 // (see wh_common.h).
 constexpr int ENC_RT = 1;  // query row tiles per wave (2 measured 414 us vs 289: 264 VGPRs, one block per CU)
-constexpr int ENC_NW = 8;  // waves per block: the K/V tile staged once for 16 * ENC_NW * ENC_RT queries
-template <typename T>
+// ENC_NW waves per block: the K/V tile staged once for 16 * ENC_NW * ENC_RT queries; 8,
+// or 4 when 8-wave blocks would give fewer than two per CU (one window: 240 -> 480 blocks)
+template <typename T, int ENC_NW>
 __global__ __launch_bounds__(64 * ENC_NW) void k_attn_enc(const T* __restrict__ qkv, int ld, int ns, int Tlen,
                                                   int64_t win_stride_in, const T* __restrict__ vt, int tkp,
                                                   T* __restrict__ out, int64_t win_stride_out) {
@@ -299,9 +300,14 @@ __global__ __launch_bounds__(64 * ENC_NW) void k_attn_enc(const T* __restrict__ 
 template <typename T>
 void launch_attn_enc(const T* qkv, int ld, int ns, int H, int Tlen, int nwin, int64_t wsi, const T* vt, int tkp, T* out,
                      int64_t wso, hipStream_t st) {
-  constexpr int QB = 16 * ENC_NW * ENC_RT;
-  dim3 grid((Tlen + QB - 1) / QB, H, nwin);
-  k_attn_enc<T><<<grid, 64 * ENC_NW, 0, st>>>(qkv, ld, ns, Tlen, wsi, vt, tkp, out, wso);
+  const int blocks8 = (Tlen + 127) / 128 * H * nwin;
+  if (blocks8 < 512) {
+    dim3 grid((Tlen + 63) / 64, H, nwin);
+    k_attn_enc<T, 4><<<grid, 256, 0, st>>>(qkv, ld, ns, Tlen, wsi, vt, tkp, out, wso);
+  } else {
+    dim3 grid((Tlen + 127) / 128, H, nwin);
+    k_attn_enc<T, 8><<<grid, 512, 0, st>>>(qkv, ld, ns, Tlen, wsi, vt, tkp, out, wso);
+  }
 }
 
 // ============================================================ decoder self-attention
