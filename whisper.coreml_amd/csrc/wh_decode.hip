@@ -331,37 +331,65 @@ __device__ __forceinline__ void lp_slice(int j, int tb, int V, int& lo, int& hi)
   hi = (int)((int64_t)tb * (j + 1) / (LP_SLICES - 1));
 }
 
+// wave-level (value desc, index asc) argbest; every lane ends with the winner
+__device__ __forceinline__ void wave_argbest(float& v, int& idx) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float ov = __shfl_xor(v, o, 64);
+    const int oi = __shfl_xor(idx, o, 64);
+    if (better(ov, oi, v, idx)) { v = ov; idx = oi; }
+  }
+}
+
+// Two barriers per workgroup: (1) after the history scan (last sampled timestamp), (2)
+// after every wave has reduced its own max, rescaled sum of exp and top-(G+1) list (or
+// argbest / Gumbel best); wave 0 then merges the 8 wave results and writes the record.
+// The slice's logits and suppress words are loaded first, before the history, so their
+// round trip overlaps it.
 __global__ __launch_bounds__(LP_THREADS) WH_LP_ATTR void k_logit_part(float* __restrict__ logits, int ldl, DecState s,
                                                            DecOpts o) {
-  __shared__ BlockRed sm;
-  __shared__ int info[4];
-  __shared__ int pmax_w[LP_THREADS / 64];
+  constexpr int NWV = LP_THREADS / 64;
+  __shared__ int pm_w[NWV], pt_w[NWV];
+  __shared__ float wmx[NWV], wse[NWV], wv_v[NWV][KC], wg_v[NWV], wg_x[NWV];
+  __shared__ int wv_i[NWV][KC], wg_i[NWV];
   const int r = blockIdx.x, j = blockIdx.y, w = r / s.G;
-  const int tid = threadIdx.x;
-  if (s.done[w]) return;
-  const int len = s.len[w], sb = s.sample_begin[w];
-  const int* hist = s.hist + (int64_t)r * s.hctx;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int V = o.V, tb = o.ts_begin;
-  {  // last timestamp token of the sampled part (decoding.py:503-508)
-    int pm = -1;
-    for (int p = sb + tid; p < len; p += LP_THREADS)
-      if (hist[p] >= tb) pm = p;
+  int lo, hi;
+  lp_slice(j, tb, V, lo, hi);
+  float* row = logits + (int64_t)r * ldl;
+  // 1. this slice's logits and suppress words (clamped addresses, masked below)
+  float xv[LP_EPT];
+  unsigned sw[LP_EPT];
 #pragma unroll
-    for (int o2 = 32; o2 > 0; o2 >>= 1) pm = max(pm, __shfl_xor(pm, o2, 64));
-    if ((tid & 63) == 0) pmax_w[tid >> 6] = pm;
+  for (int u = 0; u < LP_EPT; ++u) {
+    const int ic = min(lo + tid + LP_THREADS * u, hi - 1);
+    xv[u] = row[ic];
+    sw[u] = o.suppress ? o.suppress[ic >> 5] : 0u;
   }
-  __syncthreads();
-  if (tid == 0) {
-    const int nseq = len - sb;
-    int pm = -1;
-    for (int k = 0; k < LP_THREADS / 64; ++k) pm = max(pm, pmax_w[k]);
-    info[0] = nseq >= 1 && hist[len - 1] >= tb;
-    info[1] = nseq < 2 || hist[len - 2] >= tb;
-    info[2] = pm >= 0 ? hist[pm] : -1;
-    info[3] = (len == sb);
+  const int done = s.done[w], len = s.len[w], sb = s.sample_begin[w];
+  if (done) return;
+  // 2. history facts (decoding.py:503-508): the last timestamp token of the sampled
+  // part (len - sb <= 448 < LP_THREADS: one position per thread) and the last two tokens
+  const int* hist = s.hist + (int64_t)r * s.hctx;
+  const int p = sb + tid;
+  const int hp = hist[min(p, max(len - 1, 0))];
+  const int h1 = hist[max(len - 1, 0)], h2 = hist[max(len - 2, 0)];
+  int pm = (p < len && hp >= tb) ? p : -1, pt = hp;
+#pragma unroll
+  for (int o2 = 32; o2 > 0; o2 >>= 1) {
+    const int op = __shfl_xor(pm, o2, 64), ot = __shfl_xor(pt, o2, 64);
+    if (op > pm) { pm = op; pt = ot; }
   }
+  if (lane == 0) { pm_w[wv] = pm; pt_w[wv] = pt; }
   __syncthreads();
-  const int last_ts = info[0], penult_ts = info[1], ts_last = info[2], first = info[3];
+  int PM = -1, PT = -1;
+#pragma unroll
+  for (int k = 0; k < NWV; ++k)
+    if (pm_w[k] > PM) { PM = pm_w[k]; PT = pt_w[k]; }
+  const int nseq = len - sb;
+  const bool last_ts = nseq >= 1 && h1 >= tb, penult_ts = nseq < 2 || h2 >= tb, first = len == sb;
+  const int ts_last = PM >= 0 ? PT : -1;
   int mlo[4], mhi[4];
   int nm = 0;
   if (o.timestamps) {
@@ -379,22 +407,12 @@ __global__ __launch_bounds__(LP_THREADS) WH_LP_ATTR void k_logit_part(float* __r
     }
   }
   const bool sb_first = first && o.suppress_blank;
-  int lo, hi;
-  lp_slice(j, tb, V, lo, hi);
-  float* row = logits + (int64_t)r * ldl;
-  float xv[LP_EPT];
-  unsigned sw[LP_EPT];
-#pragma unroll
-  for (int u = 0; u < LP_EPT; ++u) {
-    const int i = lo + tid + LP_THREADS * u;
-    xv[u] = i < hi ? row[i] : -INFINITY;
-    sw[u] = (o.suppress && i < hi) ? o.suppress[i >> 5] : 0u;
-  }
+  // 3. filters in place, then this wave's max and sum of exp (online rescale across waves)
   float mx = -INFINITY;
 #pragma unroll
   for (int u = 0; u < LP_EPT; ++u) {
     const int i = lo + tid + LP_THREADS * u;
-    if (i >= hi) continue;
+    if (i >= hi) { xv[u] = -INFINITY; continue; }
     bool kill = (sw[u] >> (i & 31)) & 1u;
     if (sb_first)
       for (int b = 0; b < o.n_blank; ++b) kill |= (i == o.blank[b]);
@@ -408,15 +426,16 @@ __global__ __launch_bounds__(LP_THREADS) WH_LP_ATTR void k_logit_part(float* __r
     }
     mx = fmaxf(mx, xv[u]);
   }
-  mx = block_max(mx, sm);
-  LPRec* rec = reinterpret_cast<LPRec*>(s.lpart + ((int64_t)r * LP_SLICES + j) * LP_REC);
+  mx = wave_max(mx);
   float se = 0.f;
   if (mx > -INFINITY) {
 #pragma unroll
-    for (int u = 0; u < LP_EPT; ++u)
-      if (lo + tid + LP_THREADS * u < hi) se += __expf(xv[u] - mx);
+    for (int u = 0; u < LP_EPT; ++u) se += __expf(xv[u] - mx);  // masked entries: exp(-inf) = 0
   }
-  se = block_sum(se, sm);
+  se = wave_sum(se);
+  if (lane == 0) { wmx[wv] = mx; wse[wv] = se; }
+  LPRec* rec = reinterpret_cast<LPRec*>(s.lpart + ((int64_t)r * LP_SLICES + j) * LP_REC);
+  const int need = s.G + 1;
   if (!o.beam) {
     float bv = -INFINITY, gv = -INFINITY, gx = -INFINITY;
     int bi = 0x7fffffff, gi = 0x7fffffff;
@@ -434,66 +453,113 @@ __global__ __launch_bounds__(LP_THREADS) WH_LP_ATTR void k_logit_part(float* __r
         if (better(gsc, i, gv, gi)) { gv = gsc; gi = i; gx = x; }
       }
     }
-    block_argbest(bv, bi, sm);
+    wave_argbest(bv, bi);
     const int mine = gi;
     const float myx = gx;
-    block_argbest(gv, gi, sm);
-    __shared__ float gx_s;
-    if (mine == gi && gi != 0x7fffffff) gx_s = myx;
-    __syncthreads();
-    if (tid == 0) {
-      rec->mx = mx; rec->se = se; rec->bv = bv; rec->bi = bi;
-      rec->gv = gv; rec->gi = gi; rec->gx = gi != 0x7fffffff ? gx_s : -INFINITY;
+    wave_argbest(gv, gi);
+    const unsigned long long own = __ballot(mine == gi && gi != 0x7fffffff);
+    const float gxw = own ? __shfl(myx, __ffsll((long long)own) - 1, 64) : -INFINITY;
+    if (lane == 0) { wv_v[wv][0] = bv; wv_i[wv][0] = bi; wg_v[wv] = gv; wg_i[wv] = gi; wg_x[wv] = gxw; }
+  } else {
+    // this wave's top-(G+1) by (value desc, index asc): per-lane insertion lists, then
+    // `need` wave-level argbest rounds
+    float lv[KC];
+    int li[KC];
+#pragma unroll
+    for (int q = 0; q < KC; ++q) { lv[q] = -INFINITY; li[q] = 0x7fffffff; }
+#pragma unroll
+    for (int u = 0; u < LP_EPT; ++u) {
+      const int i = lo + tid + LP_THREADS * u;
+      if (i >= hi) continue;
+      float v = xv[u];
+      int vi = i;
+#pragma unroll
+      for (int q = 0; q < KC; ++q) {
+        if (q < need && better(v, vi, lv[q], li[q])) {
+          const float tv = lv[q]; const int ti = li[q];
+          lv[q] = v; li[q] = vi; v = tv; vi = ti;
+        }
+      }
+    }
+    int head = 0;
+    for (int q = 0; q < need; ++q) {
+      float hv = -INFINITY;
+      int hix = 0x7fffffff;
+#pragma unroll
+      for (int z = 0; z < KC; ++z)
+        if (z == head) { hv = lv[z]; hix = li[z]; }
+      float bv = hv;
+      int bi = hix;
+      wave_argbest(bv, bi);
+      if (bi == hix && bi != 0x7fffffff) ++head;
+      if (lane == 0) { wv_v[wv][q] = bv; wv_i[wv][q] = bi; }
+    }
+  }
+  __syncthreads();
+  if (wv != 0) return;
+  // 4. wave 0 merges the NWV wave results
+  float MX = -INFINITY;
+#pragma unroll
+  for (int k = 0; k < NWV; ++k) MX = fmaxf(MX, wmx[k]);
+  float SE = 0.f;
+  if (MX > -INFINITY) {
+#pragma unroll
+    for (int k = 0; k < NWV; ++k)
+      if (wmx[k] > -INFINITY) SE += wse[k] * __expf(wmx[k] - MX);
+  }
+  if (!o.beam) {
+    float bv = lane < NWV ? wv_v[lane][0] : -INFINITY, gv = lane < NWV ? wg_v[lane] : -INFINITY;
+    int bi = lane < NWV ? wv_i[lane][0] : 0x7fffffff, gi = lane < NWV ? wg_i[lane] : 0x7fffffff;
+    const float myx = lane < NWV ? wg_x[lane] : -INFINITY;
+    const int mine = gi;
+    wave_argbest(bv, bi);
+    wave_argbest(gv, gi);
+    const unsigned long long own = __ballot(mine == gi && gi != 0x7fffffff);
+    const float gx = own ? __shfl(myx, __ffsll((long long)own) - 1, 64) : -INFINITY;
+    if (lane == 0) {
+      rec->mx = MX; rec->se = SE; rec->bv = bv; rec->bi = bi;
+      rec->gv = gv; rec->gi = gi; rec->gx = gi != 0x7fffffff ? gx : -INFINITY;
     }
     return;
   }
-  // beam: the slice's top-(G+1) by (value desc, index asc): per-lane insertion lists,
-  // then need block-wide argbest rounds
-  const int need = s.G + 1;
-  float lv[KC];
-  int li[KC];
-#pragma unroll
-  for (int q = 0; q < KC; ++q) { lv[q] = -INFINITY; li[q] = 0x7fffffff; }
-#pragma unroll
-  for (int u = 0; u < LP_EPT; ++u) {
-    const int i = lo + tid + LP_THREADS * u;
-    if (i >= hi) continue;
-    float v = xv[u];
-    int vi = i;
-#pragma unroll
-    for (int q = 0; q < KC; ++q) {
-      if (q < need && better(v, vi, lv[q], li[q])) {
-        const float tv = lv[q]; const int ti = li[q];
-        lv[q] = v; li[q] = vi; v = tv; vi = ti;
-      }
-    }
+  // beam: each lane holds up to two wave candidates (NWV * need <= 72), sorted within
+  // the lane; `need` wave-level rounds take the best remaining head
+  const int c0 = lane, c1 = lane + 64, nc = NWV * need;
+  float a0 = -INFINITY, a1 = -INFINITY;
+  int i0 = 0x7fffffff, i1 = 0x7fffffff;
+  if (c0 < nc) { a0 = wv_v[c0 / need][c0 % need]; i0 = wv_i[c0 / need][c0 % need]; }
+  if (c1 < nc) { a1 = wv_v[c1 / need][c1 % need]; i1 = wv_i[c1 / need][c1 % need]; }
+  if (better(a1, i1, a0, i0)) {
+    const float tv = a0; const int ti = i0;
+    a0 = a1; i0 = i1; a1 = tv; i1 = ti;
   }
-  int head = 0;
   for (int q = 0; q < need; ++q) {
-    float hv = -INFINITY;
-    int hix = 0x7fffffff;
-#pragma unroll
-    for (int z = 0; z < KC; ++z)
-      if (z == head) { hv = lv[z]; hix = li[z]; }
-    float bv = hv;
-    int bi = hix;
-    block_argbest(bv, bi, sm);
-    if (bi == hix && bi != 0x7fffffff) ++head;
-    if (tid == 0) { rec->tv[q] = bv; rec->ti[q] = bi; }
+    float bv = a0;
+    int bi = i0;
+    wave_argbest(bv, bi);
+    if (bi == i0 && bi != 0x7fffffff) { a0 = a1; i0 = i1; a1 = -INFINITY; i1 = 0x7fffffff; }
+    if (lane == 0) { rec->tv[q] = bv; rec->ti[q] = bi; }
   }
-  if (tid == 0) { rec->mx = mx; rec->se = se; }
+  if (lane == 0) { rec->mx = MX; rec->se = SE; }
 }
 
 __global__ __launch_bounds__(64) void k_logit_combine(DecState s, DecOpts o) {
   const int r = blockIdx.x, w = r / s.G, lane = threadIdx.x;
-  if (s.done[w]) return;
-  // the row's slice records -> LDS in one round trip (the merge below reads them
-  // serially; from global memory every read would be a dependent load)
+  // the row's slice records -> LDS in one round trip, issued with the done flag's load
+  // (the merge below reads them serially; from global memory every read would be a
+  // dependent load)
   __shared__ __attribute__((aligned(16))) float recs[LP_SLICES * LP_REC];
   {
+    constexpr int N4 = LP_SLICES * LP_REC / 4, PER = (N4 + 63) / 64;
     const float4_t* src = reinterpret_cast<const float4_t*>(s.lpart + (int64_t)r * LP_SLICES * LP_REC);
     float4_t* dst = reinterpret_cast<float4_t*>(recs);
-    for (int k = lane; k < LP_SLICES * LP_REC / 4; k += 64) dst[k] = src[k];
+    float4_t v[PER];
+#pragma unroll
+    for (int k = 0; k < PER; ++k) v[k] = src[min(lane + 64 * k, N4 - 1)];
+    if (s.done[w]) return;
+#pragma unroll
+    for (int k = 0; k < PER; ++k)
+      if (lane + 64 * k < N4) dst[lane + 64 * k] = v[k];
   }
   __syncthreads();
   const LPRec* rec = reinterpret_cast<const LPRec*>(recs);
