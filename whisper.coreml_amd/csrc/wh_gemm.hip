@@ -423,6 +423,94 @@ __global__ __launch_bounds__(512) void k_gemv_rows(GemmArgs a) {
   }
 }
 
+// ============================================================ vocabulary projection, <= 32 rows
+// logits[m][n] = sum_k X[m][k] E[n][k] for a decoder step's few rows (one window's beams)
+// against the whole token embedding (V = 51866 columns, 133 MB in fp16).  X (<= 32 rows)
+// is staged in LDS once per workgroup; every WAVE then owns whole 16-column tiles (all of
+// K: no cross-wave reduction, no barrier in the loop), visiting tiles gw, gw + nwaves, ...
+// so the weight stream is split evenly over the chip's waves (12-13 tiles per CU).  Its
+// weight fragments stream in chunks of VC k-steps, the next chunk (of this tile or of the
+// wave's next tile) in flight while the current one is multiplied.
+template <typename T, int MT>
+__global__ __launch_bounds__(512) void k_vocab_small(GemmArgs a) {
+  constexpr int VC = 8;  // k-steps per chunk
+  extern __shared__ __attribute__((aligned(16))) char xsv[];
+  const int K = a.K, S = K / 32, nch = (S + VC - 1) / VC;
+  const int xrow = K * (int)sizeof(T) + 16;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = lane & 15, g = lane >> 4;
+  const T* X = reinterpret_cast<const T*>(a.X);
+  const T* W = reinterpret_cast<const T*>(a.W);
+  {  // stage X rows (rows >= M: zeros)
+    const int cpr = K * (int)sizeof(T) / 16, total = MT * 16 * cpr;
+    for (int c = tid; c < total; c += 512) {
+      const int row = c / cpr, col = c - row * cpr;
+      float4_t v = (float4_t){0.f, 0.f, 0.f, 0.f};
+      if (row < a.M) {
+        const int xr = a.x_rows ? a.x_rows[row] : row;
+        v = *reinterpret_cast<const float4_t*>(reinterpret_cast<const char*>(X + (int64_t)xr * a.ldx) + col * 16);
+      }
+      *reinterpret_cast<float4_t*>(xsv + row * xrow + col * 16) = v;
+    }
+  }
+  __syncthreads();
+  const int nt = (a.N + 15) / 16;
+  const int gw = blockIdx.x * 8 + wave, nw = gridDim.x * 8;
+  const int ntw = gw < nt ? (nt - 1 - gw) / nw + 1 : 0;  // tiles of this wave
+  const int J = ntw * nch;                                 // chunks of this wave
+  auto wsrc = [&](int j) {
+    const int t = gw + nw * (j / nch), s0 = (j % nch) * VC;
+    return W + (int64_t)min(t * 16 + r, a.N - 1) * K + s0 * 32 + 8 * g;
+  };
+  auto load_chunk = [&](int j, Frag<T>* wf) {
+    const T* wp = wsrc(j);
+    const int s0 = (j % nch) * VC;
+#pragma unroll
+    for (int c = 0; c < VC; ++c) frag_load_stream(wf[c], wp + (min(s0 + c, S - 1) - s0) * 32);
+  };
+  Frag<T> wa[VC], wb[VC];
+  float4_t acc[MT];
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt) acc[mt] = (float4_t){0.f, 0.f, 0.f, 0.f};
+  if (J > 0) load_chunk(0, wa);
+  for (int j = 0; j < J; j += 2) {
+    // chunk j in wa (chunk j+1 -> wb in flight), then chunk j+1 in wb (j+2 -> wa)
+#pragma unroll
+    for (int half = 0; half < 2; ++half) {
+      const int jj = j + half;
+      if (jj >= J) break;
+      Frag<T>* cur = half ? wb : wa;
+      Frag<T>* nxt = half ? wa : wb;
+      if (jj + 1 < J) load_chunk(jj + 1, nxt);
+      const int s0 = (jj % nch) * VC;
+#pragma unroll
+      for (int c = 0; c < VC; ++c) {
+        if (s0 + c < S) {
+#pragma unroll
+          for (int mt = 0; mt < MT; ++mt) {
+            Frag<T> xf;
+            frag_load(xf, reinterpret_cast<const T*>(xsv + (mt * 16 + r) * xrow) + (s0 + c) * 32 + 8 * g);
+            mfma_step(acc[mt], cur[c], xf);
+          }
+        }
+      }
+      if (jj % nch == nch - 1) {  // tile done: lane holds rows mt*16 + r, columns n0 + 4g .. +3
+        const int n = (gw + nw * (jj / nch)) * 16 + 4 * g;
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) {
+          const int m = mt * 16 + r;
+          if (m < a.M) {
+            float* o = a.out_f32 + (int64_t)m * a.ldo;
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+              if (n + e < a.N) o[n + e] = acc[mt][e] + (a.bias ? a.bias[n + e] : 0.f);
+          }
+          acc[mt] = (float4_t){0.f, 0.f, 0.f, 0.f};
+        }
+      }
+    }
+  }
+}
+
 // ============================================================ tall-skinny GEMM, X through LDS
 // For 33..128 rows the X operand (L2-resident activations) costs more load bandwidth
 // than the weights when every 16-column tile re-reads it.  Here a 256-thread block
@@ -610,6 +698,28 @@ int launch_gemm_tiles(const GemmArgs& a, int epi, int tile_sel, hipStream_t st) 
     const int rows_per = rows_per_block(a.M, a.mt_block);
     const int ks = epi == EPI_PARTIAL ? a.ksplit : 1;
     if (ks < 1 || ks > a.K / 32) return -4;
+    static const bool vocab_small = [] {  // WHISPER_HIP_VOCAB_SMALL=0: the k_gemv path (A/B)
+      const char* e = getenv("WHISPER_HIP_VOCAB_SMALL");
+      return !(e && e[0] == '0');
+    }();
+    if (vocab_small && epi == EPI_F32_COLS && a.N >= 16384 && a.M <= (sizeof(T) == 2 ? 32 : 16) && a.K <= 1280 &&
+        a.K % 32 == 0) {
+      const int mtv = (a.M + 15) / 16;
+      const int lds = mtv * 16 * (a.K * (int)sizeof(T) + 16);
+      const int grid = std::min(256, (a.N + 127) / 128);
+      if (mtv == 1) {
+        static bool attr1 = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_vocab_small<T, 1>),
+                                                hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024) == hipSuccess;
+        if (!attr1) return -5;
+        k_vocab_small<T, 1><<<grid, 512, lds, st>>>(a);
+      } else {
+        static bool attr2 = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_vocab_small<T, 2>),
+                                                hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024) == hipSuccess;
+        if (!attr2) return -5;
+        k_vocab_small<T, 2><<<grid, 512, lds, st>>>(a);
+      }
+      return 0;
+    }
     if (mt >= 3 && epi == EPI_F32_COLS && a.N >= 16384) {
       // vocabulary projection: NW column tiles share each staged X subchunk, so X
       // (re-read from L2 by every workgroup) costs 112/(16 NW) of the weight bytes
