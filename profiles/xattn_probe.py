@@ -18,7 +18,8 @@ audio = S.synthetic_audio(30.0 * 24, seed=1000)
 m.ctx.log_mel(audio, dims["n_mels"], padding=whisper.audio.N_SAMPLES)
 m.ctx.encode([3000 * i for i in range(24)], [3000] * 24)
 task = DecodingTask(m, whisper.DecodingOptions(language="en", beam_size=5))
-for nw in [1, 2, 4, 6, 8, 10, 12, 13, 14, 16, 18, 20, 24]:
+wins = [int(x) for x in sys.argv[2].split(",")] if len(sys.argv) > 2 else [1, 2, 4, 6, 8, 10, 12, 13, 14, 16, 18, 20, 24]
+for nw in wins:
     m.ctx.decode_begin(task.wh_opts(), [task.initial_tokens] * nw, [task.sot_index] * nw)
     xa = m.ctx.time_stage(3, 5)
     step = m.ctx.time_stage(0, 10)

@@ -1009,6 +1009,245 @@ __global__ __launch_bounds__(512, PF ? 1 : 2) void k_cross_attn1(const T* __rest
   store4(out + (int64_t)(row0 + qq) * ldo + h * 64 + dc, o[0] * inv, o[1] * inv, o[2] * inv, o[3] * inv);
 }
 
+// Balanced decoder-step cross-attention for many (window, head) pairs (256..682: 13+
+// windows at 20 heads).  One workgroup per pair puts 400 pairs (the 20-window bench
+// batch) on 256 CUs in two rounds: 144 CUs stream a second 384 KB pair while 112 idle
+// (34 us against ~29 at the chip's streaming rate, profiles/r02/xattn_probe.txt).  Here
+// every pair's 64-key tiles are cut into WPP = floor(2048 / pairs) segments at fixed
+// offsets (tiles [k NT / WPP, (k+1) NT / WPP)), one segment per wave, waves packed 8 to
+// a workgroup in (pair, segment) order: one round, <= ceil(NT / WPP) tiles per wave
+// (400 pairs: 5 segments of 4-5 tiles, 250 workgroups, <= 640 KB per CU instead of 768).
+// Each wave runs k_cross_attn1's online softmax over its tiles with the next tile's K/V
+// in flight.  Every pair is merged the same way wherever its segments ran (so identical
+// windows give bit-identical rows): M = max of the segment maxima, then
+// L = sum f_k l_k, O = sum f_k O_k in segment order.  A pair whose segments all ran in
+// this workgroup merges from LDS; a pair cut between two workgroups (<= 2 per workgroup,
+// WPP <= 8) has each segment's (O, m, l) record stored write-through (sc1) at
+// [pair][segment], drained, and the pair's counter bumped (relaxed agent atomic); the
+// workgroup drawing 1 re-arms the counter and merges the WPP records (sc1 loads).
+constexpr int XB_QPW = 4;  // pairs a workgroup may touch: ceil(8 / WPP) + 1 <= 4 for WPP >= 3
+
+template <typename T, int QZ, int TW>
+__global__ __launch_bounds__(512, 1) void k_cross_attn_bal(const T* __restrict__ q, int ldq, const T* ck, const T* cvt,
+                                                          int Tk, int H, int npair, int wpp,
+                                                          const int* __restrict__ win_row0,
+                                                          const int* __restrict__ win_nrows,
+                                                          const int* __restrict__ win_slot, int64_t win_stride, XQPart xq,
+                                                          T* __restrict__ out, int ldo) {
+  constexpr int NW = 8;
+  constexpr bool QP = QZ > 0;
+  constexpr float LOG2E = 1.4426950408889634f;
+  __shared__ float seg_m[NW][16], seg_l[NW][16];
+  __shared__ float seg_o[NW][64][17];
+  __shared__ __attribute__((aligned(16))) T qs[XB_QPW][16][72];
+  __shared__ int s_ticket[2];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int r = lane & 15, g = lane >> 4;
+  const int NT = (Tk + 63) / 64, b = blockIdx.x;
+  const int gw = b * NW + wave, nseg = npair * wpp;
+  const bool active = gw < nseg;
+  const int p = min(gw, nseg - 1) / wpp, k = min(gw, nseg - 1) - p * wpp;
+  const int t0 = k * NT / wpp, cnt = (k + 1) * NT / wpp - t0;  // this wave's tiles
+  const int pa = (b * NW) / wpp, plast = min((b * NW + NW - 1) / wpp, npair - 1);
+  const int wi = p / H, h = p - wi * H;
+  const int64_t off = (int64_t)win_slot[wi] * win_stride;
+  const T* kbase = ck + off + (int64_t)h * TKP * 64;
+  const T* vbase = cvt + off + (int64_t)h * 64 * TKP;
+  // tile i of the segment (clamped to its last: loads are never branched around)
+  auto load_kv = [&](int i, Frag<T>(&kf)[4][2], Frag<T>(&vf)[4][2]) {
+    const int kt0 = (t0 + min(i, cnt - 1)) * 64;
+#pragma unroll
+    for (int kt = 0; kt < 4; ++kt) {
+      const T* kp = kbase + (int64_t)(kt0 + kt * 16 + r) * 64 + 8 * g;
+      frag_load_stream(kf[kt][0], kp);
+      frag_load_stream(kf[kt][1], kp + 32);
+    }
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+      for (int s = 0; s < 2; ++s) frag_load_stream(vf[dt][s], vbase + (int64_t)(dt * 16 + r) * TKP + kt0 + 32 * s + 8 * g);
+  };
+  Frag<T> kf[2][4][2], vf[2][4][2];
+  load_kv(0, kf[0], vf[0]);
+  // the workgroup's pairs' query rows -> LDS (rows past the window's beams repeat its last)
+#pragma unroll
+  for (int pass = 0; pass < XB_QPW / 2; ++pass) {
+    const int j = 2 * pass + (tid >> 8), t = tid & 255;
+    const int pj = min(pa + j, plast), wj = pj / H, hj = pj - wj * H;
+    const int qq = min(t >> 4, win_nrows[wj] - 1), c = hj * 64 + (t & 15) * 4, row = win_row0[wj] + qq;
+    float4_t qv = (float4_t){0.f, 0.f, 0.f, 0.f};
+    if constexpr (QP) {
+      float4_t pp[QP ? QZ : 1];
+      const float* src = xq.part + (int64_t)row * ldq + c;
+#pragma unroll
+      for (int z = 0; z < QZ; ++z) pp[z] = load4f(src + z * xq.stride);
+      qv = load4f(xq.bias + c);
+#pragma unroll
+      for (int z = 0; z < QZ; ++z) qv += pp[z];
+    } else {
+      const T* src = q + (int64_t)row * ldq + c;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) qv[e] = (float)src[e];
+    }
+    store4(&qs[j][t >> 4][(t & 15) * 4], qv[0], qv[1], qv[2], qv[3]);
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // LDS only: K/V stay in flight
+  Frag<T> qf[2];
+  frag_load(qf[0], &qs[p - pa][r][8 * g]);
+  frag_load(qf[1], &qs[p - pa][r][32 + 8 * g]);
+
+  float m = -INFINITY, l = 0.f;
+  float4_t acc[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) acc[i] = (float4_t){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int i = 0; i < TW; ++i) {
+    const int cur = i & 1;
+    if (i + 1 < TW) load_kv(i + 1, kf[cur ^ 1], vf[cur ^ 1]);
+    if (i < cnt) {
+      const int kt0 = (t0 + i) * 64;
+      float4_t sc[4];
+#pragma unroll
+      for (int kt = 0; kt < 4; ++kt) {
+        sc[kt] = (float4_t){0.f, 0.f, 0.f, 0.f};
+        mfma_step(sc[kt], kf[cur][kt][0], qf[0]);
+        mfma_step(sc[kt], kf[cur][kt][1], qf[1]);
+      }
+      float mx = -INFINITY;
+#pragma unroll
+      for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          if (kt0 + kt * 16 + 4 * g + j >= Tk) sc[kt][j] = -INFINITY;
+          mx = fmaxf(mx, sc[kt][j]);
+        }
+      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      const float mn = fmaxf(m, mx);
+      const float sf = m == -INFINITY ? 0.f : exp2f((m - mn) * LOG2E);
+      m = mn;
+      Frag<T> pf[2];
+      float ps = 0.f;
+#pragma unroll
+      for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const float pv = exp2f((sc[kt][j] - m) * LOG2E);
+          ps += pv;
+          pf[kt >> 1].v[(kt & 1) * 4 + j] = from_f32<T>(pv);
+        }
+      ps += __shfl_xor(ps, 16, 64);
+      ps += __shfl_xor(ps, 32, 64);
+      l = l * sf + ps;
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) acc[dt] *= sf;
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt) mfma_step(acc[dt], vf[cur][dt][s], pf[s]);
+    }
+  }
+  if (g == 0) {
+    seg_m[wave][r] = m;
+    seg_l[wave][r] = l;
+  }
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) seg_o[wave][dt * 16 + 4 * g + j][r] = acc[dt][j];
+  __syncthreads();
+
+  // merge: 256 threads per pair, (row qq, 4 columns dc)
+  typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+  const auto rs = __builtin_amdgcn_make_buffer_rsrc(xq.split_rec, 0, 0x7fffffff, 0x00020000);
+  const int half = tid >> 8, t = tid & 255, qq = t >> 4, dc = (t & 15) * 4;
+  const int w0 = b * NW;  // first wave (global segment index) of this workgroup
+  auto emit = [&](int pj, float M, float L, float4_t o) {
+    const int wj = pj / H, hj = pj - wj * H;
+    if (qq < win_nrows[wj]) {
+      const float inv = 1.f / L;
+      store4(out + (int64_t)(win_row0[wj] + qq) * ldo + hj * 64 + dc, o[0] * inv, o[1] * inv, o[2] * inv, o[3] * inv);
+    }
+  };
+#pragma unroll
+  for (int pass = 0; pass < XB_QPW / 2; ++pass) {
+    const int pj = pa + 2 * pass + half;
+    if (pj <= plast) {
+      const int s0 = pj * wpp - w0, s1 = s0 + wpp;  // the pair's segments as local slots
+      if (s0 >= 0 && s1 <= NW) {                     // all here: merge from LDS
+        float M = -INFINITY;
+        for (int s = s0; s < s1; ++s) M = fmaxf(M, seg_m[s][qq]);
+        float L = 0.f;
+        float4_t o = (float4_t){0.f, 0.f, 0.f, 0.f};
+        for (int s = s0; s < s1; ++s) {
+          const float f = seg_m[s][qq] == -INFINITY ? 0.f : exp2f((seg_m[s][qq] - M) * LOG2E);
+          L += f * seg_l[s][qq];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) o[e] += f * seg_o[s][dc + e][qq];
+        }
+        emit(pj, M, L, o);
+      } else {  // cut: this workgroup's segments of the pair -> records [pair][segment]
+        for (int s = max(s0, 0); s < min(s1, NW); ++s) {
+          const int rb = (pj * wpp + (s - s0)) * XREC * 4;
+          const float4_t o = (float4_t){seg_o[s][dc][qq], seg_o[s][dc + 1][qq], seg_o[s][dc + 2][qq], seg_o[s][dc + 3][qq]};
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, o), rs, rb + (qq * 64 + dc) * 4, 0, 16);
+          if (dc == 0) {
+            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, seg_m[s][qq]), rs, rb + (1024 + qq) * 4, 0, 16);
+            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, seg_l[s][qq]), rs, rb + (1040 + qq) * 4, 0, 16);
+          }
+        }
+      }
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its records
+  __syncthreads();
+  // the cut pairs: the first if its segments began in the previous workgroup, the last
+  // if they continue in the next (distinct pairs: a workgroup holds >= 8 / WPP >= 1 whole
+  // segment runs' worth, and a pair spans <= 2 workgroups)
+  const bool cut_first = pa * wpp < w0, cut_last = plast * wpp + wpp > w0 + NW && plast != pa;
+  if (tid == 0) {
+    s_ticket[0] = cut_first ? __hip_atomic_fetch_add(xq.split_cnt + pa, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
+    s_ticket[1] = cut_last ? __hip_atomic_fetch_add(xq.split_cnt + plast, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
+  }
+  __syncthreads();
+  const int pj = half ? plast : pa;
+  if (!(half ? (cut_last && s_ticket[1] == 1) : (cut_first && s_ticket[0] == 1))) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // no instruction: keeps the loads below the add
+  if (t == 0) __hip_atomic_store(xq.split_cnt + pj, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  float4_t ov[8];
+  float mv[8], lv[8];
+#pragma unroll
+  for (int s = 0; s < 8; ++s) {  // every record load issued first (clamped index)
+    const int rb = (pj * wpp + min(s, wpp - 1)) * XREC * 4;
+    ov[s] = __builtin_bit_cast(float4_t, __builtin_amdgcn_raw_buffer_load_b128(rs, rb + (qq * 64 + dc) * 4, 0, 16));
+    mv[s] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, rb + (1024 + qq) * 4, 0, 16));
+    lv[s] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, rb + (1040 + qq) * 4, 0, 16));
+  }
+  float M = -INFINITY;
+#pragma unroll
+  for (int s = 0; s < 8; ++s)
+    if (s < wpp) M = fmaxf(M, mv[s]);
+  float L = 0.f;
+  float4_t o = (float4_t){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int s = 0; s < 8; ++s)
+    if (s < wpp) {
+      const float f = mv[s] == -INFINITY ? 0.f : exp2f((mv[s] - M) * LOG2E);
+      L += f * lv[s];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) o[e] += f * ov[s][e];
+    }
+  emit(pj, M, L, o);
+}
+
+int cross_attn_bal_enabled() {  // WHISPER_HIP_XBAL=0 keeps one workgroup per pair (A/B)
+  static const int v = [] {
+    const char* e = getenv("WHISPER_HIP_XBAL");
+    return e ? atoi(e) : 1;
+  }();
+  return v;
+}
+
 int cross_attn_split_big() {  // splits at >= 128 (window, head) pairs (WHISPER_HIP_XSPLIT_BIG, A/B)
   static const int v = [] {
     const char* e = getenv("WHISPER_HIP_XSPLIT_BIG");
@@ -1040,6 +1279,30 @@ void launch_cross_attn(const T* q, int ldq, const T* ck, const T* cv, int Tk, in
     return e ? atoi(e) : 1;
   }();
   const int ntiles = (Tk + 63) / 64;
+  // many pairs: the balanced kernel (one round, every pair cut into WPP segments)
+  const int npair = nwin * H, wpp = npair > 0 ? std::min(2048 / npair, ntiles) : 0;
+  if (one && cross_attn_bal_enabled() && xq.split_rec && xq.split_cnt && xq.max_rows >= 1 && xq.max_rows <= 16 &&
+      !qk_map && npair >= 256 && wpp >= 3 && wpp <= 8 && npair * wpp <= XREC_CAP) {
+    const int tw = (ntiles + wpp - 1) / wpp, nwg = (npair * wpp + 7) / 8;
+#define XB(QZ_, TW_)                                                                                                 \
+  k_cross_attn_bal<T, QZ_, TW_><<<nwg, 512, 0, st>>>(q, ldq, ck, cv, Tk, H, npair, wpp, win_row0, win_nrows,         \
+                                                     win_slot, win_stride, xq, out, ldo)
+#define XBZ(TW_)                  \
+  switch (xq.part ? xq.z : 0) {   \
+    case 4: XB(4, TW_); break;    \
+    case 8: XB(8, TW_); break;    \
+    case 10: XB(10, TW_); break;  \
+    default: XB(0, TW_); break;   \
+  }
+    if (tw <= 3) XBZ(3)
+    else if (tw == 4) XBZ(4)
+    else if (tw == 5) XBZ(5)
+    else if (tw <= 6) XBZ(6)
+    else XBZ(8)
+#undef XBZ
+#undef XB
+    return;
+  }
   const int nsp = xq.split_rec && xq.split_cnt ? cross_attn_splits(nwin, H) : 1;
   const int tpw = ((ntiles + nsp - 1) / nsp + 7) / 8;
   if (one && xq.max_rows >= 1 && xq.max_rows <= 16 && !qk_map && tpw <= 4) {
