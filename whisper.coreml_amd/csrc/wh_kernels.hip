@@ -414,6 +414,11 @@ void launch_self_attn(const T* q, int ldq, const T* kc, const T* vc, const int* 
 // slices in fixed order, adds the bias, writes k/v (rounded to T) into its own slot
 // at position pos and attends with them directly (no read-back of the fresh row).
 // Only valid when no other row of the launch needs this row's K/V (one row per beam).
+// Grid: one single-wave workgroup per (row, head), rows w * G + beam; the logical order
+// (window, head, beam) is laid over the XCDs in contiguous runs (xcd_remap), so the G
+// beams of one (window, head), whose ancestries mostly name the same cached (slot,
+// position) rows, run on one XCD and share its L2 (x-fastest order put them on G
+// different XCDs).
 template <typename T>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void k_self_attn_qkv(const float* __restrict__ part, int nsplit, int64_t part_stride,
                                                       const float* __restrict__ bqkv, int ns, T* __restrict__ kc,
@@ -424,7 +429,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void
   __shared__ float sc[512];
   __shared__ int slot_of[512];
   __shared__ float qs[64], vs[64];
-  const int row = blockIdx.x, h = blockIdx.y, lane = threadIdx.x;
+  const int lane = threadIdx.x, G = anc_beams;
+  const int L = xcd_remap(blockIdx.x, gridDim.x), b = L % G, wh = L / G, h = wh % H, row = (wh / H) * G + b;
   const int w = row_win[row], sl = row_slot[row], pos = row_pos[row];
   const int* an = anc + ((int64_t)w * anc_beams + sl) * ctx;
   const int64_t head_stride = (int64_t)ctx * 64;
@@ -555,8 +561,9 @@ void launch_self_attn_qkv(const float* part, int nsplit, int64_t part_stride, co
                           const int* rw, const int* rs, const int* rp, const int* anc, int anc_beams, int nbeam, int H,
                           int ctx, T* out, int ldo, int rows, hipStream_t st) {
   if (rows <= 0) return;
-  k_self_attn_qkv<T><<<dim3(rows, H), 64, 0, st>>>(part, nsplit, part_stride, bqkv, ns, kc, vc, rw, rs, rp, anc,
-                                                   anc_beams, nbeam, H, ctx, out, ldo);
+  // step rows are w * G + beam (rows % G == 0, host-checked by the caller's layout)
+  k_self_attn_qkv<T><<<rows * H, 64, 0, st>>>(part, nsplit, part_stride, bqkv, ns, kc, vc, rw, rs, rp, anc, anc_beams,
+                                             nbeam, H, ctx, out, ldo);
 }
 
 // out[m][n] = act(bias[n] + sum_z part[z][m][n]) as T (split-K epilogue of the

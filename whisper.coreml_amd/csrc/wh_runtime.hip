@@ -1234,7 +1234,11 @@ struct Ctx : public wh_ctx {
     if (!eager()) TRY(ensure_graph());
     hipEventRecord(tm.a, st);
     int steps = 0, done = 0;
-    const int chunk = 8;
+    static const int chunk = [] {  // WHISPER_HIP_POLL_CHUNK: steps per done-flag poll (A/B)
+      const char* e = getenv("WHISPER_HIP_POLL_CHUNK");
+      const int v = e ? atoi(e) : 8;
+      return v < 1 ? 1 : v;
+    }();
     // chunks of `chunk` steps, each followed by an async copy of the done flags; the
     // next chunk is queued before the host waits for the previous chunk's flags, so
     // the GPU never idles on the poll (at most one chunk of no-op steps after the last
