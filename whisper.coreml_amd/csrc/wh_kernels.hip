@@ -430,19 +430,20 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void
   __shared__ int slot_of[512];
   __shared__ float qs[64], vs[64];
   const int lane = threadIdx.x, G = anc_beams;
-  const int L = xcd_remap(blockIdx.x, gridDim.x), b = L % G, wh = L / G, h = wh % H, row = (wh / H) * G + b;
-  const int w = row_win[row], sl = row_slot[row], pos = row_pos[row];
+  // step rows: window w = row / G, beam slot = row % G (row_win / row_slot hold the same)
+  const int L = xcd_remap(blockIdx.x, gridDim.x), sl = L % G, wh = L / G, h = wh % H, w = wh / H, row = w * G + sl;
   const int* an = anc + ((int64_t)w * anc_beams + sl) * ctx;
   const int64_t head_stride = (int64_t)ctx * 64;
   const int64_t wbase = (int64_t)w * nbeam;
   auto kv_off = [&](int slot, int p) -> int64_t { return ((wbase + slot) * H + h) * head_stride + (int64_t)p * 64; };
   // one round trip for everything that does not depend on this step's projection:
-  // the ancestry slot of every cached key (8 per lane, clamped, issued together) and
-  // the q/k/v partial slabs of this row and head (lane = d)
-  const int plast = max(pos - 1, 0);
+  // the position, the ancestry slot of every context position (8 per lane, clamped to
+  // the context, issued together) and the q/k/v partial slabs of this row and head
+  // (lane = d)
+  const int pos = row_pos[row];
   int sv[8];
 #pragma unroll
-  for (int i = 0; i < 8; ++i) sv[i] = an[min(lane + 64 * i, plast)];
+  for (int i = 0; i < 8; ++i) sv[i] = an[min(lane + 64 * i, ctx - 1)];
   float qd, kd, vd;
   {
     const float* pr = part + (int64_t)row * 3 * ns + h * 64 + lane;
@@ -467,6 +468,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void
   }
   for (int i = 0; i < 8; ++i)
     if (lane + 64 * i < pos) slot_of[lane + 64 * i] = sv[i];
+  const int plast = max(pos - 1, 0);
   const T qT = from_f32<T>(qd), kT = from_f32<T>(kd), vT = from_f32<T>(vd);
   kc[kv_off(sl, pos) + lane] = kT;
   vc[kv_off(sl, pos) + lane] = vT;
@@ -479,8 +481,74 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void
   float qv[64];
 #pragma unroll
   for (int c = 0; c < 64; ++c) qv[c] = qs[c];
-  // scores of the cached positions p < pos: lane per key, two keys per lane per pass
-  // with all 16 row loads in flight (clamped addresses, no branch around a load)
+  if constexpr (sizeof(T) == 2) {
+    // passes of 128 cached keys, K and V of the pass in ONE round trip (V's addresses do
+    // not depend on the scores), online softmax across passes: K rows lane per key (two
+    // keys per lane), V lane = (key group kg, 16 B chunk dc) keys kg, kg+8, .. kg+120
+    const int kg = lane >> 3, dc = (lane & 7) * 8;
+    float m = s_cur, lsum = 0.f, o[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] = 0.f;
+    for (int p0 = 0; p0 < pos; p0 += 128) {
+      const int pa = min(p0 + lane, plast), pb = min(p0 + 64 + lane, plast);
+      const T* ra = kc + kv_off(slot_of[pa], pa);
+      const T* rb = kc + kv_off(slot_of[pb], pb);
+      Frag<T> ka[8], kb[8], vf[16];
+#pragma unroll
+      for (int c = 0; c < 8; ++c) frag_load(ka[c], ra + 8 * c);
+#pragma unroll
+      for (int c = 0; c < 8; ++c) frag_load(kb[c], rb + 8 * c);
+#pragma unroll
+      for (int u = 0; u < 16; ++u) {
+        const int pc = min(p0 + kg + 8 * u, plast);
+        frag_load(vf[u], vc + kv_off(slot_of[pc], pc) + dc);
+      }
+      __builtin_amdgcn_sched_barrier(0);  // every load of the pass ahead of the math
+      float sa = 0.f, sb = 0.f;
+#pragma unroll
+      for (int c = 0; c < 8; ++c)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          sa += qv[8 * c + e] * to_f32(ka[c].v[e]);
+          sb += qv[8 * c + e] * to_f32(kb[c].v[e]);
+        }
+      const bool va = p0 + lane < pos, vb = p0 + 64 + lane < pos;
+      const float mp = wave_max(fmaxf(va ? sa : -INFINITY, vb ? sb : -INFINITY));
+      const float mn = fmaxf(m, mp), scale = __expf(m - mn);
+      m = mn;
+      const float ea = va ? __expf(sa - m) : 0.f, eb = vb ? __expf(sb - m) : 0.f;
+      lsum = lsum * scale + wave_sum(ea + eb);
+      sc[lane] = ea;
+      sc[64 + lane] = eb;
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o[e] *= scale;
+#pragma unroll
+      for (int u = 0; u < 16; ++u) {
+        const float pw = sc[kg + 8 * u];  // 0 past the end
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o[e] += pw * to_f32(vf[u].v[e]);
+      }
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      o[e] += __shfl_xor(o[e], 8, 64);
+      o[e] += __shfl_xor(o[e], 16, 64);
+      o[e] += __shfl_xor(o[e], 32, 64);
+    }
+    if (kg == 0) {
+      const float e_cur = __expf(s_cur - m), inv = 1.f / (lsum + e_cur);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o[e] = (o[e] + e_cur * vs[dc + e]) * inv;
+      T* op = out + (int64_t)row * ldo + h * 64 + dc;
+      store4(op, o[0], o[1], o[2], o[3]);
+      store4(op + 4, o[4], o[5], o[6], o[7]);
+    }
+    return;
+  }
+  // fp32 (parity context): scores of the cached positions p < pos: lane per key, two
+  // keys per lane per pass with all 16 row loads in flight (clamped addresses, no branch
+  // around a load), then P.V
   float mx = s_cur;
   for (int p0 = 0; p0 < pos; p0 += 128) {
     const int pa = min(p0 + lane, plast), pb = min(p0 + 64 + lane, plast);
