@@ -80,6 +80,28 @@ WH_DEV void mfma_step(float4_t& acc, const Frag<float>& a, const Frag<float>& b)
   for (int j = 0; j < 8; ++j) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.v[j], b.v[j], acc, 0, 0, 0);
 }
 
+// ---------------------------------------------------------------- write-through stores
+// Outputs the NEXT launch reads (split-K slabs, logits) are stored write-through (sc1):
+// the kernel-end release then has no dirty L2 lines to write back, which otherwise
+// lengthens the boundary by ~bytes / 6 TB/s (MI355X_MICROARCH.md price list,
+// "boundary"; 100-row step: 3.68 -> 3.55 ms with the k_proj slabs write-through).
+// base must be wave-uniform (a kernel argument); offsets in bytes, < 2^31.
+#ifndef WH_WT
+#define WH_WT 1
+#endif
+typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
+WH_DEV auto wt_rsrc(const void* base) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, 0x7fffffff, 0x00020000);
+}
+template <typename R>
+WH_DEV void wt_store1(R rs, int off, float v) {
+  __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), rs, off, 0, 16);
+}
+template <typename R>
+WH_DEV void wt_store4(R rs, int off, float4_t v) {
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, v), rs, off, 0, 16);
+}
+
 // ---------------------------------------------------------------- conversions
 template <typename T> WH_DEV T from_f32(float x);
 template <> WH_DEV float from_f32<float>(float x) { return x; }

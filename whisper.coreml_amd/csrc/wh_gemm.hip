@@ -499,10 +499,17 @@ __global__ __launch_bounds__(512) void k_vocab_small(GemmArgs a) {
         for (int mt = 0; mt < MT; ++mt) {
           const int m = mt * 16 + r;
           if (m < a.M) {
+#if WH_WT
+            const auto rs = wt_rsrc(a.out_f32);
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+              if (n + e < a.N) wt_store1(rs, (m * a.ldo + n + e) * 4, acc[mt][e] + (a.bias ? a.bias[n + e] : 0.f));
+#else
             float* o = a.out_f32 + (int64_t)m * a.ldo;
 #pragma unroll
             for (int e = 0; e < 4; ++e)
               if (n + e < a.N) o[n + e] = acc[mt][e] + (a.bias ? a.bias[n + e] : 0.f);
+#endif
           }
           acc[mt] = (float4_t){0.f, 0.f, 0.f, 0.f};
         }
@@ -604,14 +611,25 @@ __global__ __launch_bounds__(64 * NW) void k_gemv_x(GemmArgs a) {
     if (m >= a.M || n >= a.N) continue;
     float4_t v = acc[mt];
     if (EPI == EPI_F32_COLS) {
+#if WH_WT
+      const auto rs = wt_rsrc(a.out_f32);
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if (n + j < a.N) wt_store1(rs, (m * a.ldo + n + j) * 4, v[j] + (a.bias ? a.bias[n + j] : 0.f));
+#else
       float* o = a.out_f32 + (int64_t)m * a.ldo;
 #pragma unroll
       for (int j = 0; j < 4; ++j)
         if (n + j < a.N) o[n + j] = v[j] + (a.bias ? a.bias[n + j] : 0.f);
+#endif
       continue;
     }
     if (EPI == EPI_PARTIAL) {
+#if WH_WT
+      wt_store4(wt_rsrc(a.out_f32), (int)((((int64_t)kz * a.M + m) * a.ldo + n) * 4), v);
+#else
       store4(a.out_f32 + ((int64_t)kz * a.M + m) * a.ldo + n, v[0], v[1], v[2], v[3]);
+#endif
       continue;
     }
     if (a.bias) v += load4f(a.bias + n);

@@ -134,7 +134,12 @@ __global__ __launch_bounds__(64 * NSUB * KW) void k_proj(GemmArgs a) {
     if (m >= a.M) continue;
     float4_t v = acc[mt];
     if constexpr (EPI == EPI_PARTIAL) {
+#if WH_WT
+      // write-through (sc1): the slab leaves no dirty L2 lines for the kernel-end release
+      wt_store4(wt_rsrc(a.out_f32), (int)((((int64_t)kz * a.M + m) * a.ldo + n) * 4), v);
+#else
       store4(a.out_f32 + ((int64_t)kz * a.M + m) * a.ldo + n, v[0], v[1], v[2], v[3]);
+#endif
     } else if constexpr (EPI == EPI_F32_COLS) {
       float* o = a.out_f32 + (int64_t)m * a.ldo;
 #pragma unroll
