@@ -33,7 +33,8 @@ KERNELS = {
     # short name -> regex on the mangled kernel name
     "k_proj": r"k_projIDF16_",                # fp16 split-K projections (all tile variants), 100 rows
     "k_proj1": r"k_proj1IDF16_",              # single-window projections (5 rows, all six shapes)
-    "k_cross_attn1": r"k_cross_attn1IDF16_",  # the step's cross-attention, 20 windows (no key split)
+    "k_cross_attn1": r"k_cross_attn1IDF16_",  # the step's cross-attention, <= 12 windows
+    "k_cross_attn_bal": r"k_cross_attn_balIDF16_",  # the step's cross-attention, 13+ windows (20: bench)
     "k_gemm_256": r"k_gemm_256",              # encoder GEMMs of the 20-window encode (all epilogues)
 }
 
