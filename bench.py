@@ -125,6 +125,14 @@ def projection_bytes_per_launch(dims, rows, elem=2):
     return tot // len(shapes)
 
 
+def xattn_kernel(dims, n_windows):
+    """The step cross-attention kernel wh_kernels.hip:launch_cross_attn picks: the
+    balanced one-round form at 256..682 (window, head) pairs, else one workgroup per
+    pair (with a key split below 128 pairs)."""
+    pairs = n_windows * dims["n_text_head"]
+    return "k_cross_attn_bal" if 256 <= pairs and 3 <= 2048 // pairs else "k_cross_attn1"
+
+
 def cross_attn_bytes_per_launch(dims, n_windows, rows, elem=2):
     """One layer's cross-attention: K and V of every window (2*1500*n) + q in / out."""
     n = dims["n_text_state"]
@@ -352,7 +360,7 @@ def main():
                      "timing": "HIP events around each launch inside eager decoder steps",
                      "ms_per_launch_back_to_back": round(gemv_b2b_ms, 5)},
         "roofline_overall": overall,
-        "roofline_cross_attn": {"bound": "hbm", "kernel": f"k_cross_attn1 ({n_win} windows x {args.beam} beams)",
+        "roofline_cross_attn": {"bound": "hbm", "kernel": f"{xattn_kernel(dims, n_win)} ({n_win} windows x {args.beam} beams)",
                                 "achieved": round(gbs(xattn_bytes, xattn_ms), 1), "peak": HBM_PEAK_GBS,
                                 "frac": round(gbs(xattn_bytes, xattn_ms) / HBM_PEAK_GBS, 4),
                                 "bytes_per_launch": xattn_bytes, "ms_per_launch": round(xattn_ms, 5)},
