@@ -419,33 +419,19 @@ void launch_self_attn(const T* q, int ldq, const T* kc, const T* vc, const int* 
 // beams of one (window, head), whose ancestries mostly name the same cached (slot,
 // position) rows, run on one XCD and share its L2 (x-fastest order put them on G
 // different XCDs).
-// Up to SA_WPB independent waves per workgroup, each with its own LDS slice, no block
-// barrier anywhere: at >= 1024 (row, head) waves, 4 per workgroup (a quarter of the
-// workgroups to dispatch, ~2 per CU: 100-row step 3.68 -> 3.59 ms); fewer waves keep one
-// per workgroup so they spread over the CUs.
-#ifndef WH_SA_WPB
-#define WH_SA_WPB 4
-#endif
-constexpr int SA_WPB = WH_SA_WPB;
 template <typename T>
-__global__ __launch_bounds__(64 * SA_WPB) __attribute__((amdgpu_waves_per_eu(1, 2))) void k_self_attn_qkv(const float* __restrict__ part, int nsplit, int64_t part_stride,
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void k_self_attn_qkv(const float* __restrict__ part, int nsplit, int64_t part_stride,
                                                       const float* __restrict__ bqkv, int ns, T* __restrict__ kc,
                                                       T* __restrict__ vc, const int* __restrict__ row_win,
                                                       const int* __restrict__ row_slot, const int* __restrict__ row_pos,
                                                       const int* __restrict__ anc, int anc_beams, int nbeam, int H,
-                                                      int ctx, T* __restrict__ out, int ldo, int npairs) {
-  __shared__ float sc_all[SA_WPB][512];
-  __shared__ int slot_all[SA_WPB][512];
-  __shared__ float qs_all[SA_WPB][64], vs_all[SA_WPB][64];
-  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63, G = anc_beams;
-  float* sc = sc_all[wv];
-  int* slot_of = slot_all[wv];
-  float* qs = qs_all[wv];
-  float* vs = vs_all[wv];
+                                                      int ctx, T* __restrict__ out, int ldo) {
+  __shared__ float sc[512];
+  __shared__ int slot_of[512];
+  __shared__ float qs[64], vs[64];
+  const int lane = threadIdx.x, G = anc_beams;
   // step rows: window w = row / G, beam slot = row % G (row_win / row_slot hold the same)
-  const int L = xcd_remap(blockIdx.x, gridDim.x) * (int)(blockDim.x >> 6) + wv;
-  if (L >= npairs) return;
-  const int sl = L % G, wh = L / G, h = wh % H, w = wh / H, row = w * G + sl;
+  const int L = xcd_remap(blockIdx.x, gridDim.x), sl = L % G, wh = L / G, h = wh % H, w = wh / H, row = w * G + sl;
   const int* an = anc + ((int64_t)w * anc_beams + sl) * ctx;
   const int64_t head_stride = (int64_t)ctx * 64;
   const int64_t wbase = (int64_t)w * nbeam;
@@ -489,7 +475,7 @@ __global__ __launch_bounds__(64 * SA_WPB) __attribute__((amdgpu_waves_per_eu(1, 
   qs[lane] = to_f32(qT);
   vs[lane] = to_f32(vT);
   const float s_cur = wave_sum(to_f32(qT) * to_f32(kT));
-  // each wave owns its LDS slice: its writes are visible to all its lanes once they have
+  // the block is one wave: its LDS writes are visible to all its lanes once they have
   // completed (no barrier, and no wait for the K/V row stores above)
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   float qv[64];
@@ -644,9 +630,8 @@ void launch_self_attn_qkv(const float* part, int nsplit, int64_t part_stride, co
                           int ctx, T* out, int ldo, int rows, hipStream_t st) {
   if (rows <= 0) return;
   // step rows are w * G + beam (rows % G == 0, host-checked by the caller's layout)
-  const int np = rows * H, wpb = np >= 1024 ? SA_WPB : 1;
-  k_self_attn_qkv<T><<<(np + wpb - 1) / wpb, 64 * wpb, 0, st>>>(part, nsplit, part_stride, bqkv, ns, kc, vc, rw, rs, rp,
-                                                                anc, anc_beams, nbeam, H, ctx, out, ldo, np);
+  k_self_attn_qkv<T><<<rows * H, 64, 0, st>>>(part, nsplit, part_stride, bqkv, ns, kc, vc, rw, rs, rp, anc, anc_beams,
+                                             nbeam, H, ctx, out, ldo);
 }
 
 // out[m][n] = act(bias[n] + sum_z part[z][m][n]) as T (split-K epilogue of the
