@@ -99,22 +99,15 @@ def decoder_step_bytes(dims, n_windows, beams, mean_ctx, elem=2):
     return weights + cross + selfkv
 
 
-def p1_path(rows):
-    """The decoder step at <= 8 rows runs k_proj1 (whole-K projections with fused
-    LayerNorm prologues and epilogues: wh_runtime.hip dec_layers_p1) unless
-    WHISPER_HIP_P1=0; larger batches run the split-K k_proj."""
-    return rows <= 8 and os.environ.get("WHISPER_HIP_P1", "1") != "0"
-
-
-def projection_bytes_per_launch(dims, rows, elem=2):
+def projection_bytes_per_launch(dims, rows, p1, elem=2):
     """Algorithmic bytes of one decoder-step projection, averaged over the six per
     decoder layer (qkv n->3n, out n->n, cross-q n->n, cross-out n->n, fc1 n->4n,
     fc2 4n->n).  Split-K k_proj: weights N*K + activations rows*K (fp16) + fp32 result
-    rows*N.  k_proj1 (p1_path): weights N*K; the LayerNorm'd projections read the fp32
+    rows*N.  k_proj1 (`p1`): weights N*K; the LayerNorm'd projections read the fp32
     residual rows*K*4 + gamma/beta and write rows*N fp16; the residual ones read
     rows*K fp16 and read + write the fp32 residual rows*N*4*2."""
     n = dims["n_text_state"]
-    if p1_path(rows):
+    if p1:
         ln = [(3 * n, n), (n, n), (4 * n, n)]
         res = [(n, n), (n, n), (n, 4 * n)]
         tot = sum(N * K * elem + rows * K * 4 + 2 * K * 4 + rows * N * elem for N, K in ln)
@@ -123,14 +116,6 @@ def projection_bytes_per_launch(dims, rows, elem=2):
     shapes = [(3 * n, n), (n, n), (n, n), (n, n), (4 * n, n), (n, 4 * n)]
     tot = sum(N * K * elem + rows * K * elem + rows * N * 4 for N, K in shapes)
     return tot // len(shapes)
-
-
-def xattn_kernel(dims, n_windows):
-    """The step cross-attention kernel wh_kernels.hip:launch_cross_attn picks: the
-    balanced one-round form at 256..682 (window, head) pairs, else one workgroup per
-    pair (with a key split below 128 pairs)."""
-    pairs = n_windows * dims["n_text_head"]
-    return "k_cross_attn_bal" if 256 <= pairs and 3 <= 2048 // pairs else "k_cross_attn1"
 
 
 def cross_attn_bytes_per_launch(dims, n_windows, rows, elem=2):
@@ -170,6 +155,12 @@ def cpu_baseline(model_name, sd, audio, beams, n_steps):
     from oracle import ref_whisper as R
     from whisper import synthetic as S
     threads = torch.get_num_threads()
+    cpu_model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            cpu_model = next(line.split(":", 1)[1].strip() for line in f if line.startswith("model name"))
+    except (OSError, StopIteration):
+        pass
     dims = S.MODEL_DIMS[model_name]
     m = R.OracleWhisper(dims, sd)
     st = R.SpecialTokens.for_model(dims)
@@ -184,10 +175,11 @@ def cpu_baseline(model_name, sd, audio, beams, n_steps):
     steps = n_steps or 224
     per_window = t_enc + t_dec * (224 / steps)
     kind = "the whole window" if not n_steps else f"{steps} steps scaled to 224"
-    return dict(value=round(30.0 / per_window, 4), unit="xRT (audio-s/s)", cores=threads, kind="port",
+    return dict(value=round(30.0 / per_window, 4), unit="xRT (audio-s/s)", cores=threads, cpu_model=cpu_model,
+                kind="port",
                 sample=f"1 window (30 s) of {model_name}, beam {beams}, {kind}: encoder {t_enc:.1f} s + decode "
                        f"{t_dec:.1f} s ({len(res.tokens)} tokens; oracle/ref_whisper.py decode with the reference's "
-                       f"beam search, torch CPU fp32, {threads} threads)")
+                       f"beam search, torch CPU fp32, {threads} threads of {cpu_model})")
 
 
 def main():
@@ -296,7 +288,9 @@ def main():
     # back-to-back: the same launches queued without their producers (time_stage 2)
     gemv_ms = model.ctx.time_stage(7, 3)
     gemv_b2b_ms = model.ctx.time_stage(2, 3)
-    gemv_bytes = projection_bytes_per_launch(dims, rows)
+    kern = model.ctx.step_kernels(n_win, args.beam)  # what the library runs for this batch
+    p1 = kern["proj"] == "k_proj1"
+    gemv_bytes = projection_bytes_per_launch(dims, rows, p1)
     xattn_ms = model.ctx.time_stage(3, 3)
     xattn_bytes = cross_attn_bytes_per_launch(dims, n_win, rows)
     step_ms = model.ctx.time_stage(0, 20)
@@ -323,7 +317,7 @@ def main():
     def gbs(b, ms):
         return b / (ms * 1e-3) / 1e9
 
-    traffic = load_traffic("k_proj1" if p1_path(rows) else "k_proj")
+    traffic = load_traffic(kern["proj"])
     parallel = (f"one {file_seconds:.0f} s file sharded over {world} GPU(s) by 30 s clips (whisper/distributed.py): "
                 f"RCCL all-reduce(max) of the log-mel maximum + gather of the segment records")
     out = {
@@ -352,7 +346,7 @@ def main():
         "encoder_ms_per_window": round(enc_ms / max(enc_windows, 1), 3),
         "encoder_tflops": round(encoder_flops(dims) * enc_windows / (enc_ms * 1e-3) / 1e12, 1) if enc_ms else None,
         "roofline": {"bound": "hbm", "kernel": (f"k_proj1 whole-K projection, fused LayerNorm / epilogue ({rows} rows"
-                                                if p1_path(rows) else f"k_proj split-K projection ({rows} rows")
+                                                if p1 else f"k_proj split-K projection ({rows} rows")
                                                + ", avg of the six per decoder layer)",
                      "achieved": round(gbs(gemv_bytes, gemv_ms), 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(gbs(gemv_bytes, gemv_ms) / HBM_PEAK_GBS, 4),
@@ -360,7 +354,7 @@ def main():
                      "timing": "HIP events around each launch inside eager decoder steps",
                      "ms_per_launch_back_to_back": round(gemv_b2b_ms, 5)},
         "roofline_overall": overall,
-        "roofline_cross_attn": {"bound": "hbm", "kernel": f"{xattn_kernel(dims, n_win)} ({n_win} windows x {args.beam} beams)",
+        "roofline_cross_attn": {"bound": "hbm", "kernel": f"{kern['xattn']} ({n_win} windows x {args.beam} beams)",
                                 "achieved": round(gbs(xattn_bytes, xattn_ms), 1), "peak": HBM_PEAK_GBS,
                                 "frac": round(gbs(xattn_bytes, xattn_ms) / HBM_PEAK_GBS, 4),
                                 "bytes_per_launch": xattn_bytes, "ms_per_launch": round(xattn_ms, 5)},

@@ -178,6 +178,11 @@ int wh_align_batch(wh_ctx* ctx, int n_win, const int* slots, const int* tokens, 
    path [2][n_rows + n_cols], *path_len valid entries of each */
 int wh_dtw(wh_ctx* ctx, const float* x, int n_rows, int n_cols, int* path, int* path_len);
 
+/* the kernels the decoder step runs for a batch of n_win windows x group rows, as
+   "proj=<name>,xattn=<name>" (the dominant projection family and the cross-attention;
+   what bench.py labels its roofline lines with).  Returns the length written. */
+int wh_step_kernels(wh_ctx* ctx, int n_win, int group, char* buf, int cap);
+
 /* cumulative stage wall times in ms: [0] mel [1] encode [2] prefill [3] steps
    [4] step count [5] encode windows */
 int wh_stats(wh_ctx* ctx, double* out, int n);

@@ -158,6 +158,97 @@ def step_goldens(name: str, seed: int = 0, audio_seed: int = 1, mixed_seeds=(2, 
     np.savez_compressed(os.path.join(OUT, f"{name}_steps.npz"), **out)
 
 
+def step_goldens_mixed(name: str, seed: int = 0, audio_seeds=(2, 3, 4)):
+    """Teacher-forced beam trajectories of further audio windows, so that a co-batched
+    teacher-forced test holds every window of a mixed batch to its own reference
+    trajectory (the kernel-selection branches by window count: wh_kernels.hip
+    launch_cross_attn, wh_proj.hip launch_proj_partial)."""
+    t0 = time.time()
+    model, _ = build_ref_model(name, seed)
+    dims = syn.MODEL_DIMS[name]
+    eot = 50257 if dims["n_vocab"] >= 51865 else 50256
+    out = {"seed": np.int32(seed), "audio_seeds": np.asarray(audio_seeds, np.int32)}
+    for s in audio_seeds:
+        audio = syn.synthetic_audio(30.0, seed=s)
+        mel = ref_audio.log_mel_spectrogram(audio, dims["n_mels"], padding=N_SAMPLES)
+        seg = ref_audio.pad_or_trim(mel[:, :3000], 3000)
+        rec = StepRecorder()
+        r = refw.decode(model, seg, ref_decoding.DecodingOptions(
+            temperature=0.0, beam_size=5, suppress_tokens=f"-1,{eot}", language="en", fp16=False))
+        rec.close()
+        rec.pack(f"s{s}_tf_beam_fixed", out)
+        out[f"s{s}_tf_beam_fixed_tokens"] = np.asarray(r.tokens, dtype=np.int32)
+        print(f"[{name}] mixed steps seed {s}: {len(rec.tok)} calls {time.time()-t0:.1f}s", flush=True)
+    np.savez_compressed(os.path.join(OUT, f"{name}_steps_mixed.npz"), **out)
+
+
+def prefix_goldens(names=("micro", "tiny.en")):
+    """DecodingOptions(prefix=...) at the default sample_len (max_prefix_len = 0: Python's
+    [-0:] keeps the WHOLE prefix, decoding.py:620-626), at sample_len = 200 (keeps the
+    last 24 tokens) and 300 (max_prefix_len = -76: drops the FIRST 76), plus a string
+    prefix; greedy and beam 5, natural decoding."""
+    res = {}
+    for name in names:
+        model, _ = build_ref_model(name)
+        dims = syn.MODEL_DIMS[name]
+        audio = syn.synthetic_audio(30.0, seed=1)
+        mel = ref_audio.log_mel_spectrogram(audio, dims["n_mels"], padding=N_SAMPLES)
+        seg = ref_audio.pad_or_trim(mel[:, :3000], 3000)
+        pre = [int(t) for t in np.random.default_rng(9).integers(300, 20000, 100)]
+        cases = {
+            "list_default": dict(prefix=pre),
+            "list_len200": dict(prefix=pre, sample_len=200),
+            "list_len300": dict(prefix=pre, sample_len=300),
+            "str_default": dict(prefix="And so my fellow Americans"),
+            "list_default_beam": dict(prefix=pre[:30], beam_size=5),
+            "prompt_prefix": dict(prefix=pre[:12], prompt=list(range(1000, 1040))),
+        }
+        out = {}
+        for key, kw in cases.items():
+            t0 = time.time()
+            r = refw.decode(model, seg, ref_decoding.DecodingOptions(temperature=0.0, language="en", fp16=False, **kw))
+            out[key] = dict(options={k: v for k, v in kw.items()}, tokens=[int(t) for t in r.tokens],
+                            avg_logprob=float(r.avg_logprob), no_speech_prob=float(r.no_speech_prob))
+            print(f"[{name}] prefix {key}: {len(r.tokens)} tok {time.time()-t0:.1f}s", flush=True)
+        res[name] = dict(seed=0, audio_seed=1, cases=out)
+        del model
+    with open(os.path.join(OUT, "prefix.json"), "w") as f:
+        json.dump(res, f, indent=0)
+
+
+def words_beam_goldens(name: str = "large-v3"):
+    """Config 5 as specified (beam 5 + word timestamps) at real dims: the reference's
+    transcribe(..., beam_size=5, word_timestamps=True) on the 65 s clip grid, merged
+    into <name>_words.json next to the greedy run."""
+    import base64
+    model, _ = build_ref_model(name)
+    path = os.path.join(OUT, f"{name}_words.json")
+    with open(path) as f:
+        res = json.load(f)
+    dims = syn.MODEL_DIMS[name]
+    tok = ref_tok.get_tokenizer(dims["n_vocab"] >= 51865, num_languages=dims["n_vocab"] - 51765 -
+                                int(dims["n_vocab"] >= 51865), language="en", task="transcribe")
+    audio = syn.synthetic_audio(res["audio_seconds"], seed=res["audio_seed"])
+    kw = dict(beam_size=5, condition_on_previous_text=False, clip_timestamps="0,30,30,60,60", word_timestamps=True)
+    t0 = time.time()
+    out = refw.transcribe(model, audio, temperature=0.0, language="en", fp16=False, verbose=None, **kw)
+    segs, ids = [], set()
+    for s_ in out["segments"]:
+        ids.update(int(t) for t in s_["tokens"])
+        segs.append(dict(seek=s_["seek"], start=s_["start"], end=s_["end"], tokens=[int(t) for t in s_["tokens"]],
+                         words=[dict(word=w["word"], start=w["start"], end=w["end"],
+                                     probability=float(w["probability"])) for w in s_.get("words", [])]))
+    res["runs"]["clip_beam_words"] = kw
+    res["segments"]["clip_beam_words"] = segs
+    dec = tok.encoding._decoder
+    for i in sorted(ids):
+        if i < tok.eot:
+            res["token_bytes"][str(i)] = base64.b64encode(dec[i]).decode()
+    print(f"[{name}] transcribe clip_beam_words: {len(segs)} segs {time.time()-t0:.1f}s", flush=True)
+    with open(path, "w") as f:
+        json.dump(res, f, indent=0)
+
+
 def pack_result(prefix: str, r, out: dict):
     out[f"{prefix}_tokens"] = np.asarray(r.tokens, dtype=np.int32)
     out[f"{prefix}_avg_logprob"] = np.float64(r.avg_logprob)
@@ -470,6 +561,12 @@ def main(argv):
             dtw_goldens()
         elif w == "assets":
             asset_export()
+        elif w == "prefix":
+            prefix_goldens()
+        elif w.endswith("_steps_mixed"):
+            step_goldens_mixed(w[:-len("_steps_mixed")])
+        elif w.endswith("_words_beam"):
+            words_beam_goldens(w[:-len("_words_beam")])
         elif w.endswith("_words"):
             base = w[:-len("_words")]
             model, _ = build_ref_model(base)

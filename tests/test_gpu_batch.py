@@ -87,34 +87,41 @@ def test_bench_batch_fp16_slots_identical():
     assert len(first) == len(g["beam_fixed_tokens"])
 
 
-def _teacher_force(m, gs, kind, n_win):
-    """Replays the reference trajectory `kind` through the per-step ABI on n_win
-    copies of the golden window; returns per-(step, row) relative errors and the
-    per-step top-1 agreement where the reference's top-2 margin is decisive."""
-    tok = gs[f"tf_{kind}_tok"]            # [S][G]
-    topv, topi = gs[f"tf_{kind}_topv"], gs[f"tf_{kind}_topi"]   # [S][G][K]
-    src = gs[f"tf_{kind}_src"] if f"tf_{kind}_src" in gs.files else None
-    S, G = tok.shape
-    sot = [int(t) for t in np.load(os.path.join(GOLDEN, f"{m.name}.npz"))["sot_sequence"]]
-    assert sot[-1] == int(tok[0, 0])
+def _trajectory(gs, prefix):
+    """One reference trajectory: per step the rows' input tokens, the top-32 of the raw
+    logits, and (beam) the reorder source rows."""
+    return dict(tok=gs[f"{prefix}_tok"], topv=gs[f"{prefix}_topv"], topi=gs[f"{prefix}_topi"],
+                src=gs[f"{prefix}_src"] if f"{prefix}_src" in gs.files else None)
+
+
+def _teacher_force(m, trajs, sot):
+    """Replays one reference trajectory per window (trajs[w]) through the per-step ABI:
+    wh_prefill of the sot sequence, then per step the reorder (beam) and wh_step with the
+    reference's tokens.  Returns per-(step, row) relative errors and the per-step top-1
+    agreement where the reference's top-2 margin is decisive."""
+    n_win = len(trajs)
+    S, G = trajs[0]["tok"].shape
+    for t in trajs:
+        assert t["tok"].shape == (S, G) and sot[-1] == int(t["tok"][0, 0])
     two = m.ctx.prefill([sot] * n_win, G, [0] * n_win)         # [n_win][2][V]
     rel = np.zeros((S, n_win * G))
     top1 = np.ones((S, n_win * G), dtype=bool)
-    rng = topv[..., 0] - topv[..., -1]
 
     def score(s, rows):
         for r in range(n_win * G):
-            b = r % G
-            got = rows[r][topi[s, b]]
-            rel[s, r] = np.abs(got - topv[s, b]).max() / rng[s, b]
-            if topv[s, b, 0] - topv[s, b, 1] > 2 * TAU[m.dtype] * rng[s, b]:
-                top1[s, r] = int(np.argmax(rows[r])) == int(topi[s, b, 0])
+            w, b = divmod(r, G)
+            topv, topi = trajs[w]["topv"][s, b], trajs[w]["topi"][s, b]
+            rng = topv[0] - topv[-1]
+            rel[s, r] = np.abs(rows[r][topi] - topv).max() / rng
+            if topv[0] - topv[1] > 2 * TAU[m.dtype] * rng:
+                top1[s, r] = int(np.argmax(rows[r])) == int(topi[0])
 
     score(0, np.repeat(two[:, 1], G, axis=0))
     for s in range(1, S):
-        if src is not None:
-            m.ctx.reorder_kv([w * G + int(x) for w in range(n_win) for x in src[s - 1]])
-        lg = m.ctx.step([int(x) for _ in range(n_win) for x in tok[s]], text_offsets=[len(sot) + s - 1] * n_win)
+        if trajs[0]["src"] is not None:
+            m.ctx.reorder_kv([w * G + int(x) for w in range(n_win) for x in trajs[w]["src"][s - 1]])
+        lg = m.ctx.step([int(x) for w in range(n_win) for x in trajs[w]["tok"][s]],
+                        text_offsets=[len(sot) + s - 1] * n_win)
         score(s, lg)
     return rel, top1
 
@@ -139,22 +146,48 @@ def test_teacher_forced_few_windows(dtype, n_win):
     _teacher_forced_case("large-v3", dtype, "beam_fixed", n_win)
 
 
-def _teacher_forced_case(name, dtype, kind, n_win):
+def _teacher_forced_case(name, dtype, kind, n_win, mixed=False):
+    """n_win windows through the teacher-forced step: copies of the golden window, or
+    (mixed) windows of four different audio seeds cycled, each held to its own
+    reference trajectory (tests/golden/<name>_steps_mixed.npz)."""
     gs = _steps(name)
     m = full_model(name, dtype)
     assert m.dtype == dtype
-    m.ctx.mel_write(np.concatenate([golden_window(name)] * n_win, axis=1))
+    sot = [int(t) for t in np.load(os.path.join(GOLDEN, f"{name}.npz"))["sot_sequence"]]
+    if mixed:
+        gm = np.load(os.path.join(GOLDEN, f"{name}_steps_mixed.npz"))
+        seeds = [int(gs["audio_seed"])] + [int(x) for x in gm["audio_seeds"]]
+        tr = {seeds[0]: _trajectory(gs, f"tf_{kind}")}
+        tr.update({sd: _trajectory(gm, f"s{sd}_tf_{kind}") for sd in seeds[1:]})
+        order = [seeds[w % len(seeds)] for w in range(n_win)]
+        mel = np.concatenate([golden_window(name, sd) for sd in order], axis=1)
+        trajs = [tr[sd] for sd in order]
+    else:
+        mel = np.concatenate([golden_window(name)] * n_win, axis=1)
+        trajs = [_trajectory(gs, f"tf_{kind}")] * n_win
+    m.ctx.mel_write(mel)
     m.ctx.encode([3000 * i for i in range(n_win)], [3000] * n_win)
-    rel, top1 = _teacher_force(m, gs, kind, n_win)
+    rel, top1 = _teacher_force(m, trajs, sot)
     worst = np.unravel_index(int(np.argmax(rel)), rel.shape)
-    print(f"{name} {dtype} {kind} rows={rel.shape[1]}: max rel err {rel.max():.3e} at step {worst[0]} row {worst[1]}, "
-          f"p99 {np.quantile(rel, 0.99):.3e}, mean {rel.mean():.3e}; top-1 agreement {top1.mean():.4f}")
+    print(f"{name} {dtype} {kind} rows={rel.shape[1]}{' mixed' if mixed else ''}: max rel err {rel.max():.3e} at step "
+          f"{worst[0]} row {worst[1]}, p99 {np.quantile(rel, 0.99):.3e}, mean {rel.mean():.3e}; "
+          f"top-1 agreement {top1.mean():.4f}")
     assert rel.max() <= TAU[dtype], f"max rel err {rel.max():.3e} > {TAU[dtype]}"
     assert top1.all(), f"top-1 differs at {np.argwhere(~top1)[:5].tolist()} despite a decisive margin"
-    # every window of the batch is held to the bound on its own (the step cross-attention
-    # cuts windows at different key tiles, so identical windows agree to rounding only)
+    # every window of the batch is held to the bound on its own
     per_win = rel.reshape(rel.shape[0], n_win, -1).max(axis=(0, 2))
     assert (per_win <= TAU[dtype]).all(), per_win
+
+
+@pytest.mark.parametrize("n_win", [4, 6, 8, 13, 15, 17])
+@pytest.mark.parametrize("dtype", ["fp16", "fp32"])
+def test_teacher_forced_mixed_windows(dtype, n_win):
+    """large-v3 beam-5 trajectories of four different audio windows, cycled over n_win
+    windows (20 - 85 rows): every step kernel's selection by batch shape runs against the
+    reference (cross-attention segment distribution, k_proj tilings and split counts,
+    token selection rows); 15 windows is config 4's per-rank batch (3600 s over 8 GPUs).
+    Reference: decoder.py:241-327, decoding.py:350-409."""
+    _teacher_forced_case("large-v3", dtype, "beam_fixed", n_win, mixed=True)
 
 
 @pytest.mark.parametrize("name", ["micro", "large-v3"])
@@ -186,4 +219,28 @@ def test_reference_host_loop_drives_step_abi(name):
     np.testing.assert_array_equal(np.asarray(res.tokens), g["beam_fixed_tokens"])
     assert res.avg_logprob == pytest.approx(float(g["beam_fixed_avg_logprob"]), abs=1e-3)
     if name == "micro":
+        m.close()
+
+
+def test_failed_prefill_leaves_no_batch():
+    """A wh_prefill that fails (here: an initial token outside the vocabulary) leaves no
+    usable per-step batch: the previous batch's wh_step / wh_reorder_kv are refused
+    instead of running on a half-written ancestry / KV table (wh_runtime.hip
+    begin_batch)."""
+    import whisper
+    from whisper.backend_hip import HipBackendError
+    m = whisper.load_model("micro", device=0, dtype="fp32", max_windows=2, max_group=5, synthetic=True)
+    try:
+        m.ctx.mel_write(golden_window("micro"))
+        m.ctx.encode([0], [3000])
+        sot = [int(t) for t in np.load(os.path.join(GOLDEN, "micro.npz"))["sot_sequence"]]
+        m.ctx.prefill([sot], 5, [0])
+        m.ctx.step([sot[-1]] * 5, text_offsets=[len(sot)])
+        with pytest.raises(HipBackendError):
+            m.ctx.prefill([sot[:-1] + [10 ** 6]], 5, [0])
+        with pytest.raises(HipBackendError, match="no per-step batch"):
+            m.ctx.step([sot[-1]] * 5)
+        with pytest.raises(HipBackendError, match="no per-step batch"):
+            m.ctx.reorder_kv(list(range(5)))
+    finally:
         m.close()

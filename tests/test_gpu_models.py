@@ -74,6 +74,80 @@ def test_fp32_tokens_exact(name, kind):
     assert res.avg_logprob == pytest.approx(float(g[f"{kind}_avg_logprob"]), abs=1e-3)
 
 
+NATURAL = [(n, k) for n in MODELS for k in ("greedy", "greedy_prompt", "greedy_notime")] + [("tiny.en", "beam")]
+
+
+def _natural_options(kind):
+    """The reference runs behind the natural goldens (oracle/gen_golden.py model_goldens):
+    EOT allowed, timestamps on unless `notime`, a 40-token prompt for `prompt`."""
+    opts = dict(language="en")
+    if kind == "greedy_prompt":
+        opts["prompt"] = list(range(1000, 1040))
+    if kind == "greedy_notime":
+        opts["without_timestamps"] = True
+    if kind == "beam":
+        opts["beam_size"] = 5
+    return opts
+
+
+@pytest.mark.parametrize("name,kind", NATURAL)
+def test_fp32_natural_tokens_exact(name, kind):
+    """Natural decoding (EOT may win, decoding.py:707-737) at real dims, fp32: tokens equal
+    the reference's, including the prompt prefill at real width (<|startofprev|> + 40
+    tokens + sot sequence, decoding.py:628-638) and the no-timestamp sot sequence."""
+    import whisper
+    g = _golden(name)
+    m = _model(name, "fp32")
+    res = whisper.decode(m, _window(name), whisper.DecodingOptions(**_natural_options(kind)))
+    np.testing.assert_array_equal(np.asarray(res.tokens), g[f"{kind}_tokens"])
+    assert res.avg_logprob == pytest.approx(float(g[f"{kind}_avg_logprob"]), abs=1e-3)
+    assert res.no_speech_prob == pytest.approx(float(g[f"{kind}_no_speech_prob"]), abs=1e-4)
+
+
+@pytest.mark.parametrize("dtype", ["fp16", "fp32"])
+@pytest.mark.parametrize("name", MODELS)
+def test_prompt_prefill_logits(name, dtype):
+    """First pass over a 44-token prompted sequence: the last row's logits against the
+    reference's top-64 (same bars as test_first_step_logits)."""
+    g = _golden(name)
+    m = _model(name, dtype)
+    m.ctx.mel_write(_window(name))
+    m.ctx.encode([0], [3000])
+    logits, _ = m.ctx.prefill_logits(0, [int(t) for t in g["prompt_tokens"]])
+    row = logits[-1]
+    topi, topv = g["prompt_last_topi"], g["prompt_last_topv"]
+    rng = float(topv.max() - topv.min())
+    err = float(np.abs(row[topi] - topv).max())
+    print(f"{name} {dtype}: prompt prefill top-64 max abs err {err:.3e} (range {rng:.2f})")
+    assert err < (1e-3 * rng if dtype == "fp32" else 0.02 * rng)
+    assert int(np.argmax(row)) == int(topi[0])
+
+
+@pytest.mark.parametrize("name", MODELS)
+def test_fp16_natural_greedy_agreement(name):
+    """fp16 natural greedy equals the reference through every step whose post-filter top-2
+    margin (recorded by the reference run, greedy_margins) exceeds twice the fp16
+    teacher-forced bound, taken in absolute terms as TAU * the median top-32 range of
+    the reference's steps."""
+    import whisper
+    from test_gpu_batch import TAU, _steps
+    g = _golden(name)
+    m = _model(name, "fp16")
+    res = whisper.decode(m, _window(name), whisper.DecodingOptions(language="en"))
+    got, ref = np.asarray(res.tokens), g["greedy_tokens"]
+    topv = _steps(name)["tf_greedy_fixed_topv"][:, 0]
+    eps = TAU["fp16"] * float(np.median(topv[:, 0] - topv[:, -1]))
+    margins = g["greedy_margins"]
+    close = margins <= 2 * eps
+    need = int(np.argmax(close)) if close.any() else len(margins)
+    n = min(len(got), len(ref))
+    agree = int(np.argmax(got[:n] != ref[:n])) if np.any(got[:n] != ref[:n]) else n
+    print(f"{name} fp16 natural greedy agreement {agree}/{len(ref)} (decisive prefix {need})")
+    assert agree >= min(need, len(ref))
+    if need >= len(margins):
+        np.testing.assert_array_equal(got, ref)
+
+
 @pytest.mark.parametrize("name", MODELS)
 def test_fp16_greedy_agreement(name):
     """fp16 greedy (free running, fixed work) equals the reference through every step

@@ -27,6 +27,23 @@ typedef float float8_t __attribute__((ext_vector_type(8)));
 
 #define WH_DEV __device__ __forceinline__
 
+// Tuning switches (WHISPER_HIP_* environment variables that select measured-but-not-
+// adopted kernel variants for A/B runs) are read only by the tuning build
+// (`make tune` -> lib/libwhisper_hip_tune.so, loaded with WHISPER_HIP_LIB).  The shipped
+// library ignores the environment: every variant it can run is the tested default.
+#ifndef WH_TUNING
+#define WH_TUNING 0
+#endif
+#include <stdlib.h>
+static inline const char* tune_env(const char* name) {
+#if WH_TUNING
+  return getenv(name);
+#else
+  (void)name;
+  return nullptr;
+#endif
+}
+
 // ---------------------------------------------------------------- fragments
 template <typename T> struct Frag;
 template <> struct Frag<half_t> { half8_t v; };

@@ -626,7 +626,7 @@ void launch_logit_rows(float* logits, int ldl, const DecState& s, const DecOpts&
   // the sliced selection (k_logit_part + k_logit_combine) unless WHISPER_HIP_LOGIT_SPLIT=0
   // (config 2, turbo one window: 0.380 -> 0.346 ms per token; config 3 unchanged)
   static const bool split = [] {
-    const char* e = getenv("WHISPER_HIP_LOGIT_SPLIT");
+    const char* e = tune_env("WHISPER_HIP_LOGIT_SPLIT");
     return !(e && e[0] == '0');
   }();
   const int slice_max = (o.ts_begin + LP_SLICES - 2) / (LP_SLICES - 1);

@@ -648,7 +648,7 @@ int gemv_ksplit(int M, int N, int K, int max_z, int mt_block) {
   // k-range at these sizes, so the wall time is one block's latency as long as the
   // blocks fit on the CUs at once: take the largest z with blocks <= the target
   // (default 256 = one per CU; WHISPER_HIP_GEMV_WGS overrides for tuning).
-  const char* env = getenv("WHISPER_HIP_GEMV_WGS");
+  const char* env = tune_env("WHISPER_HIP_GEMV_WGS");
   const int target = env ? atoi(env) : 256;
   const int mt = (M + 15) / 16;
   const bool xpath = mt >= 3;  // k_gemv_x (EPI_PARTIAL with >= 33 rows)
@@ -668,7 +668,7 @@ int launch_gemm_tiles(const GemmArgs& a, int epi, int tile_sel, hipStream_t st);
 template <typename T>
 int launch_gemm(const GemmArgs& a, int epi, hipStream_t st) {
   static const int tile_sel = [] {  // WHISPER_HIP_GEMM=128 keeps the 128x128 kernel (A/B)
-    const char* e = getenv("WHISPER_HIP_GEMM");
+    const char* e = tune_env("WHISPER_HIP_GEMM");
     return e ? atoi(e) : 256;
   }();
   return launch_gemm_tiles<T>(a, epi, tile_sel, st);
@@ -717,7 +717,7 @@ int launch_gemm_tiles(const GemmArgs& a, int epi, int tile_sel, hipStream_t st) 
     const int ks = epi == EPI_PARTIAL ? a.ksplit : 1;
     if (ks < 1 || ks > a.K / 32) return -4;
     static const bool vocab_small = [] {  // WHISPER_HIP_VOCAB_SMALL=0: the k_gemv path (A/B)
-      const char* e = getenv("WHISPER_HIP_VOCAB_SMALL");
+      const char* e = tune_env("WHISPER_HIP_VOCAB_SMALL");
       return !(e && e[0] == '0');
     }();
     if (vocab_small && epi == EPI_F32_COLS && a.N >= 16384 && a.M <= (sizeof(T) == 2 ? 32 : 16) && a.K <= 1280 &&
@@ -742,7 +742,7 @@ int launch_gemm_tiles(const GemmArgs& a, int epi, int tile_sel, hipStream_t st) 
       // vocabulary projection: NW column tiles share each staged X subchunk, so X
       // (re-read from L2 by every workgroup) costs 112/(16 NW) of the weight bytes
       static const int nw = [] {
-        const char* e = getenv("WHISPER_HIP_VOCAB_WAVES");
+        const char* e = tune_env("WHISPER_HIP_VOCAB_WAVES");
         const int v = e ? atoi(e) : 8;
         return v == 4 ? 4 : 8;  // 16 waves spill
       }();

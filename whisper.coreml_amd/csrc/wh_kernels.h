@@ -20,7 +20,7 @@ void launch_self_attn(const T* q, int ldq, const T* kc, const T* vc, const int* 
                       const int* anc, int anc_beams, int nbeam, int H, int ctx, T* out, int ldo, int rows,
                       hipStream_t st);
 template <typename T>
-void launch_self_attn_qkv(const float* part, int nsplit, int64_t part_stride, const float* bqkv, int ns, T* kc, T* vc,
+int launch_self_attn_qkv(const float* part, int nsplit, int64_t part_stride, const float* bqkv, int ns, T* kc, T* vc,
                           const int* rw, const int* rs, const int* rp, const int* anc, int anc_beams, int nbeam, int H,
                           int ctx, T* out, int ldo, int rows, hipStream_t st);
 template <typename T>
@@ -35,27 +35,23 @@ struct XQPart {
   int z = 0;
   const float* bias = nullptr;
   int max_rows = 0;  // rows per window when known (decoder step: the beam group)
-  // k_cross_attn1 key split (few windows): per-split records [win][head][split][XREC]
-  // and one arrival counter per (window, head), zero between launches; null = no split
+  // step cross-attention records of pairs cut between workgroups, [pair][segment][XREC],
+  // one arrival counter per (window, head) pair (zero between launches), and the pair
+  // capacity of both; null = the first-pass kernel
   float* split_rec = nullptr;
   int* split_cnt = nullptr;
+  int max_pairs = 0;
 };
-constexpr int XREC = 16 * 64 + 32;  // floats per split record: O[16][64], m[16], l[16]
-constexpr int XSPLIT_MAX = 8;
-// key splits per (window, head) for the step cross-attention: spread the keys of few
-// windows over ~256 workgroups (1 window: 20 workgroups would leave 236 CUs idle);
-// WHISPER_HIP_XSPLIT caps it (A/B; 1 = no split)
-constexpr int XREC_CAP = 2048;  // split records allocated per context
-int cross_attn_split_cap();
-int cross_attn_split_big();
-inline int cross_attn_splits(int nwin, int H) {
-  const int pairs = nwin * H;
-  int s = pairs >= 128 ? cross_attn_split_big() : 256 / pairs;
-  const int cap = cross_attn_split_cap();
-  if (s > cap) s = cap;
-  s = s < 1 ? 1 : s > XSPLIT_MAX ? XSPLIT_MAX : s;
-  return pairs * s <= XREC_CAP ? s : 1;
-}
+constexpr int XREC = 16 * 64 + 32;  // floats per segment record: O[16][64], m[16], l[16]
+// step cross-attention segments (k_xattn_seg): XS_T key tiles of 64 per segment, at
+// most XS_NSP segments per (window, head) pair (Tk <= XS_NSP * XS_T * 64 = 1536), at
+// most XS_SMAX segments per workgroup, at most XS_QP pairs per workgroup's range
+constexpr int XS_T = 2;
+constexpr int XS_NSP = 12;
+constexpr int XS_SMAX = 24;
+constexpr int XS_QP = 4;
+static_assert((XS_SMAX + XS_NSP - 1) / XS_NSP + 1 <= XS_QP, "pairs per workgroup range");
+int xattn_seg_grid(int npair, int nsp);
 inline bool cross_attn_q_slabs(int z) { return z == 4 || z == 8 || z == 10; }
 template <typename T>
 void launch_cross_attn(const T* q, int ldq, const T* ck, const T* cv, int Tk, int H, int nsplit, int nwin,

@@ -625,13 +625,15 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void
 }
 
 template <typename T>
-void launch_self_attn_qkv(const float* part, int nsplit, int64_t part_stride, const float* bqkv, int ns, T* kc, T* vc,
+int launch_self_attn_qkv(const float* part, int nsplit, int64_t part_stride, const float* bqkv, int ns, T* kc, T* vc,
                           const int* rw, const int* rs, const int* rp, const int* anc, int anc_beams, int nbeam, int H,
                           int ctx, T* out, int ldo, int rows, hipStream_t st) {
-  if (rows <= 0) return;
-  // step rows are w * G + beam (rows % G == 0, host-checked by the caller's layout)
+  if (rows <= 0) return 0;
+  // the kernel takes window and beam from the row index: step rows are w * G + beam
+  if (anc_beams < 1 || rows % anc_beams) return -1;
   k_self_attn_qkv<T><<<rows * H, 64, 0, st>>>(part, nsplit, part_stride, bqkv, ns, kc, vc, rw, rs, rp, anc, anc_beams,
                                              nbeam, H, ctx, out, ldo);
+  return 0;
 }
 
 // out[m][n] = act(bias[n] + sum_z part[z][m][n]) as T (split-K epilogue of the
@@ -853,284 +855,76 @@ __global__ __launch_bounds__(64) void k_cross_combine(const float* __restrict__ 
   out[(int64_t)row * ldo + h * 64 + lane] = from_f32<T>(num / den);
 }
 
-// Decoder-step variant: one workgroup per (window, head, key split); without a split
-// (gridDim.z == 1, many windows) it covers all keys, so there is no partial and no
-// k_cross_combine launch.  8 waves; wave w takes the split's tiles w, w+8, ... (split s
-// of S owns the tiles t = s + S*j) with an online softmax, the next tile's K/V fragments
-// in flight while the current tile is computed; the 8 waves' (m, l, O) are merged in
-// LDS.  S == 1: the normalised rows are written as T.  S > 1 (few windows: the keys of
-// one window's 20 heads spread over ~160 workgroups instead of 20): each split writes
-// its (O, m, l) record write-through (sc1), drains it and adds to the (window, head)
-// counter (relaxed agent atomic); the workgroup drawing S-1 re-arms the counter and
-// combines the S records in split order (sc1 loads; deterministic for any arrival
-// order; cdna_hip_programming.md §6 Guideline 16 R1).  <= 16 rows per window (beams of
-// a step), query from q or reduced from split-K slabs (QZ > 0).
-template <typename T, int QZ, int TPW, int PF>
-__global__ __launch_bounds__(512, PF ? 1 : 2) void k_cross_attn1(const T* __restrict__ q, int ldq, const T* ck, const T* cvt,
-                                                     int Tk, const int* __restrict__ win_row0,
-                                                     const int* __restrict__ win_nrows, const int* __restrict__ win_slot,
-                                                     int64_t win_stride, XQPart xq, T* __restrict__ out, int ldo) {
-  constexpr int NW = 8;
-  constexpr bool QP = QZ > 0;
-  constexpr float LOG2E = 1.4426950408889634f;
-  __shared__ float red_m[NW][16], red_l[NW][16];
-  __shared__ float red_o[NW][64][17];
-  __shared__ __attribute__((aligned(16))) T qs[32][72];
-  __shared__ int s_ticket;
-  const int wi = blockIdx.x, h = blockIdx.y, H = gridDim.y, S = gridDim.z, sp = blockIdx.z;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int r = lane & 15, g = lane >> 4;
-  const int row0 = win_row0[wi], nrows = win_nrows[wi];
-  const int ntiles = (Tk + 63) / 64;
-  const T* kbase = ck + (int64_t)win_slot[wi] * win_stride + (int64_t)h * TKP * 64;
-  const T* vbase = cvt + (int64_t)win_slot[wi] * win_stride + (int64_t)h * 64 * TKP;
-  // loads are never branched around (a branch turns the compiler's counted waits into
-  // full drains): tiles past the end reload the wave's first tile and skip the math
-  auto load_kv = [&](int it, Frag<T> (&kf)[4][2], Frag<T> (&vf)[4][2]) {
-    const int t = sp + S * (wave + NW * it), kt0 = (t < ntiles ? t : sp) * 64;
-#pragma unroll
-    for (int kt = 0; kt < 4; ++kt) {
-      const T* kp = kbase + (int64_t)(kt0 + kt * 16 + r) * 64 + 8 * g;
-      frag_load_stream(kf[kt][0], kp);
-      frag_load_stream(kf[kt][1], kp + 32);
-    }
-#pragma unroll
-    for (int dt = 0; dt < 4; ++dt)
-#pragma unroll
-      for (int s = 0; s < 2; ++s) frag_load_stream(vf[dt][s], vbase + (int64_t)(dt * 16 + r) * TKP + kt0 + 32 * s + 8 * g);
-  };
-  // PF 1: the next tile's fragments load while this tile computes (2 register sets,
-  // one workgroup per CU); PF 2: every tile of the wave is loaded up front (one HBM
-  // round trip per workgroup); PF 0: one set, two workgroups per CU hide each other
-  constexpr int NSET = PF == 2 ? TPW : PF == 1 ? 2 : 1;
-  Frag<T> kf[NSET][4][2], vf[NSET][4][2];
-  load_kv(0, kf[0], vf[0]);
-  if constexpr (PF == 2) {
-#pragma unroll
-    for (int it = 1; it < TPW; ++it) load_kv(it, kf[it], vf[it]);
-  }
-  // the query rows -> LDS
-  float4_t qv = (float4_t){0.f, 0.f, 0.f, 0.f};
-  {
-    const int t = tid & 255, qq = min(t >> 4, nrows - 1), c = h * 64 + (t & 15) * 4;
-    if constexpr (QP) {
-      float4_t pp[QP ? QZ : 1];
-      const float* src = xq.part + (int64_t)(row0 + qq) * ldq + c;
-#pragma unroll
-      for (int z = 0; z < QZ; ++z) pp[z] = load4f(src + z * xq.stride);
-      qv = load4f(xq.bias + c);
-#pragma unroll
-      for (int z = 0; z < QZ; ++z) qv += pp[z];
-    } else {
-      const T* src = q + (int64_t)(row0 + qq) * ldq + c;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) qv[e] = (float)src[e];
-    }
-  }
-  store4(&qs[tid >> 4][(tid & 15) * 4], qv[0], qv[1], qv[2], qv[3]);
-  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // LDS only: K/V stay in flight
-  const int qr = min(r, nrows - 1);
-  Frag<T> qf[2];
-  frag_load(qf[0], &qs[qr][8 * g]);
-  frag_load(qf[1], &qs[qr][32 + 8 * g]);
+// ------------------------------------------------------------ step cross-attention
+// Decoder-step cross-attention (decoder.py:74-91 for the step's query rows: <= 16 rows
+// per window, the beams), batch-invariant and balanced over the chip.
+//
+// Numerics are fixed per (window, head) pair, whatever the batch: the pair's 64-key
+// tiles form nsp = ceil(Tk / 64) / XS_T segments of XS_T tiles; a segment's online
+// softmax runs over its tiles in order, and the pair's nsp (m, l, O) records are merged
+// in segment order by xs_merge.  How many windows share the launch changes only which
+// workgroup computes a segment and where it is merged, never an arithmetic operation,
+// so a window's output is bit-identical in any batch.
+//
+// Work distribution (speed only): the segments of all pairs, in (pair, segment) order,
+// are dealt in contiguous ranges to nwg workgroups (<= 256: one per CU, each range
+// <= XS_SMAX segments); the workgroup's 8 waves take its segments round-robin, each
+// with the next tile's K and V in flight (the last segment of a wave is peeled, so no
+// load is clamped or wasted).  A pair whose segments are all in the workgroup merges
+// from LDS.  A pair cut between workgroups has this workgroup's records stored
+// write-through (sc1) at [pair][segment], drained by every storing wave, and counted on
+// the pair's arrival counter (relaxed agent atomic, + the segments contributed); the
+// workgroup that completes the count re-arms it and merges all records with sc1 loads
+// (cdna_hip_programming.md §6 Guideline 16 R1, MI355X_MICROARCH.md "Valid forms").
+// K: [slot][head][TKP][64]; V transposed [slot][head][64][TKP] with the 32-key
+// permutation, so both MFMA operands load straight from HBM into fragments.
+constexpr float XS_LOG2E = 1.4426950408889634f;
 
-  float m = -INFINITY, l = 0.f;
-  float4_t acc[4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) acc[i] = (float4_t){0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-  for (int it = 0; it < TPW; ++it) {
-    const int cur = PF == 2 ? it : PF == 1 ? (it & 1) : 0;
-    if constexpr (PF == 1) {
-      if (it + 1 < TPW) load_kv(it + 1, kf[cur ^ 1], vf[cur ^ 1]);
-    } else if constexpr (PF == 0) {
-      if (it > 0) load_kv(it, kf[0], vf[0]);
-    }
-    const int t = sp + S * (wave + NW * it);
-    if (t < ntiles) {
-      const int kt0 = t * 64;
-      float4_t sc[4];
-#pragma unroll
-      for (int kt = 0; kt < 4; ++kt) {
-        sc[kt] = (float4_t){0.f, 0.f, 0.f, 0.f};
-        mfma_step(sc[kt], kf[cur][kt][0], qf[0]);
-        mfma_step(sc[kt], kf[cur][kt][1], qf[1]);
-      }
-      float mx = -INFINITY;
-#pragma unroll
-      for (int kt = 0; kt < 4; ++kt)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          if (kt0 + kt * 16 + 4 * g + j >= Tk) sc[kt][j] = -INFINITY;
-          mx = fmaxf(mx, sc[kt][j]);
-        }
-      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-      const float mn = fmaxf(m, mx);
-      const float sf = m == -INFINITY ? 0.f : exp2f((m - mn) * LOG2E);
-      m = mn;
-      Frag<T> pf[2];
-      float ps = 0.f;
-#pragma unroll
-      for (int kt = 0; kt < 4; ++kt)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const float p = exp2f((sc[kt][j] - m) * LOG2E);
-          ps += p;
-          pf[kt >> 1].v[(kt & 1) * 4 + j] = from_f32<T>(p);
-        }
-      ps += __shfl_xor(ps, 16, 64);
-      ps += __shfl_xor(ps, 32, 64);
-      l = l * sf + ps;
-#pragma unroll
-      for (int dt = 0; dt < 4; ++dt) acc[dt] *= sf;
-#pragma unroll
-      for (int s = 0; s < 2; ++s)
-#pragma unroll
-        for (int dt = 0; dt < 4; ++dt) mfma_step(acc[dt], vf[cur][dt][s], pf[s]);
-    }
-  }
-  // merge the 8 waves (lanes of every g hold the row stats of q = r)
-  if (g == 0) {
-    red_m[wave][r] = m;
-    red_l[wave][r] = l;
-  }
-#pragma unroll
-  for (int dt = 0; dt < 4; ++dt)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) red_o[wave][dt * 16 + 4 * g + j][r] = acc[dt][j];
-  __syncthreads();
-  const int qq = tid >> 4, dc = (tid & 15) * 4;
-  if (S == 1) {
-    if (tid < 256 && qq < nrows) {
-      float M = -INFINITY;
-#pragma unroll
-      for (int w = 0; w < NW; ++w) M = fmaxf(M, red_m[w][qq]);
-      float f[NW], L = 0.f;
-#pragma unroll
-      for (int w = 0; w < NW; ++w) {
-        f[w] = red_m[w][qq] == -INFINITY ? 0.f : exp2f((red_m[w][qq] - M) * LOG2E);
-        L += f[w] * red_l[w][qq];
-      }
-      const float inv = 1.f / L;
-      float o[4];
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        o[e] = 0.f;
-#pragma unroll
-        for (int w = 0; w < NW; ++w) o[e] += f[w] * red_o[w][dc + e][qq];
-        o[e] *= inv;
-      }
-      store4(out + (int64_t)(row0 + qq) * ldo + h * 64 + dc, o[0], o[1], o[2], o[3]);
-    }
-    return;
-  }
-  // split: this split's (O unnormalised, m, l) record, write-through
-  typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
-  const auto rs = __builtin_amdgcn_make_buffer_rsrc(xq.split_rec, 0, 0x7fffffff, 0x00020000);
-  const int pair = wi * H + h;
-  if (tid < 256) {
-    float M = -INFINITY;
-#pragma unroll
-    for (int w = 0; w < NW; ++w) M = fmaxf(M, red_m[w][qq]);
-    float f[NW], L = 0.f;
-#pragma unroll
-    for (int w = 0; w < NW; ++w) {
-      f[w] = red_m[w][qq] == -INFINITY ? 0.f : exp2f((red_m[w][qq] - M) * LOG2E);
-      L += f[w] * red_l[w][qq];
-    }
-    float4_t o = (float4_t){0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int e = 0; e < 4; ++e)
-#pragma unroll
-      for (int w = 0; w < NW; ++w) o[e] += f[w] * red_o[w][dc + e][qq];
-    const int rb = (pair * S + sp) * XREC * 4;  // record byte offset
-    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, o), rs, rb + (qq * 64 + dc) * 4, 0, 16);
-    if (dc == 0) {
-      __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, M), rs, rb + (1024 + qq) * 4, 0, 16);
-      __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, L), rs, rb + (1040 + qq) * 4, 0, 16);
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its stores
-  }
-  __syncthreads();
-  if (tid == 0) s_ticket = __hip_atomic_fetch_add(xq.split_cnt + pair, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  __syncthreads();
-  if (s_ticket != S - 1) return;
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // no instruction: keeps the loads below the add
-  if (tid == 0) __hip_atomic_store(xq.split_cnt + pair, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  if (tid >= 256 || qq >= nrows) return;
-  float4_t ov[XSPLIT_MAX];
-  float mv[XSPLIT_MAX], lv[XSPLIT_MAX];
-#pragma unroll
-  for (int s = 0; s < XSPLIT_MAX; ++s) {  // every record load issued first (clamped index)
-    const int rb = (pair * S + min(s, S - 1)) * XREC * 4;
-    ov[s] = __builtin_bit_cast(float4_t, __builtin_amdgcn_raw_buffer_load_b128(rs, rb + (qq * 64 + dc) * 4, 0, 16));
-    mv[s] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, rb + (1024 + qq) * 4, 0, 16));
-    lv[s] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, rb + (1040 + qq) * 4, 0, 16));
-  }
+// the pair merge, shared by the LDS and the record path (identical operations)
+WH_DEV float4_t xs_merge(int n, const float (&mv)[XS_NSP], const float (&lv)[XS_NSP], const float4_t (&ov)[XS_NSP]) {
   float M = -INFINITY;
 #pragma unroll
-  for (int s = 0; s < XSPLIT_MAX; ++s)
-    if (s < S) M = fmaxf(M, mv[s]);
+  for (int k = 0; k < XS_NSP; ++k)
+    if (k < n) M = fmaxf(M, mv[k]);
   float L = 0.f;
   float4_t o = (float4_t){0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-  for (int s = 0; s < XSPLIT_MAX; ++s) {
-    const float f = (s < S && mv[s] != -INFINITY) ? exp2f((mv[s] - M) * LOG2E) : 0.f;
-    L += f * lv[s];
-    o += f * ov[s];
-  }
+  for (int k = 0; k < XS_NSP; ++k)
+    if (k < n) {
+      const float f = mv[k] == -INFINITY ? 0.f : exp2f((mv[k] - M) * XS_LOG2E);
+      L = __builtin_fmaf(f, lv[k], L);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) o[e] = __builtin_fmaf(f, ov[k][e], o[e]);
+    }
   const float inv = 1.f / L;
-  store4(out + (int64_t)(row0 + qq) * ldo + h * 64 + dc, o[0] * inv, o[1] * inv, o[2] * inv, o[3] * inv);
+  return o * inv;
 }
 
-// Balanced decoder-step cross-attention for many (window, head) pairs (256..682: 13+
-// windows at 20 heads).  One workgroup per pair puts 400 pairs (the 20-window bench
-// batch) on 256 CUs in two rounds: 144 CUs stream a second 384 KB pair while 112 idle
-// (34 us against ~29 at the chip's streaming rate, profiles/r02/xattn_probe.txt).  Here
-// every pair's 64-key tiles are cut into WPP = floor(2048 / pairs) segments at fixed
-// offsets (tiles [k NT / WPP, (k+1) NT / WPP)), one segment per wave, waves packed 8 to
-// a workgroup in (pair, segment) order: one round, <= ceil(NT / WPP) tiles per wave
-// (400 pairs: 5 segments of 4-5 tiles, 250 workgroups, <= 640 KB per CU instead of 768).
-// Each wave runs k_cross_attn1's online softmax over its tiles with the next tile's K/V
-// in flight.  Every pair is merged the same way wherever its segments ran (so identical
-// windows give bit-identical rows): M = max of the segment maxima, then
-// L = sum f_k l_k, O = sum f_k O_k in segment order.  A pair whose segments all ran in
-// this workgroup merges from LDS; a pair cut between two workgroups (<= 2 per workgroup,
-// WPP <= 8) has each segment's (O, m, l) record stored write-through (sc1) at
-// [pair][segment], drained, and the pair's counter bumped (relaxed agent atomic); the
-// workgroup drawing 1 re-arms the counter and merges the WPP records (sc1 loads).
-constexpr int XB_QPW = 4;  // pairs a workgroup may touch: ceil(8 / WPP) + 1 <= 4 for WPP >= 3
-
-template <typename T, int QZ, int TW>
-__global__ __launch_bounds__(512, 1) void k_cross_attn_bal(const T* __restrict__ q, int ldq, const T* ck, const T* cvt,
-                                                          int Tk, int H, int npair, int wpp,
-                                                          const int* __restrict__ win_row0,
-                                                          const int* __restrict__ win_nrows,
-                                                          const int* __restrict__ win_slot, int64_t win_stride, XQPart xq,
-                                                          T* __restrict__ out, int ldo) {
+template <typename T, int QZ>
+__global__ __launch_bounds__(512, 1) void k_xattn_seg(const T* __restrict__ q, int ldq, const T* ck, const T* cvt, int Tk,
+                                                     int H, int npair, int nsp, const int* __restrict__ win_row0,
+                                                     const int* __restrict__ win_nrows,
+                                                     const int* __restrict__ win_slot, int64_t win_stride, XQPart xq,
+                                                     T* __restrict__ out, int ldo) {
   constexpr int NW = 8;
   constexpr bool QP = QZ > 0;
-  constexpr float LOG2E = 1.4426950408889634f;
-  __shared__ float seg_m[NW][16], seg_l[NW][16];
-  __shared__ float seg_o[NW][64][17];
-  __shared__ __attribute__((aligned(16))) T qs[XB_QPW][16][72];
+  __shared__ float seg_m[XS_SMAX][16], seg_l[XS_SMAX][16];
+  __shared__ float seg_o[XS_SMAX][64][17];
+  __shared__ __attribute__((aligned(16))) T qs[XS_QP][16][72];
   __shared__ int s_ticket[2];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int r = lane & 15, g = lane >> 4;
-  const int NT = (Tk + 63) / 64, b = blockIdx.x;
-  const int gw = b * NW + wave, nseg = npair * wpp;
-  const bool active = gw < nseg;
-  const int p = min(gw, nseg - 1) / wpp, k = min(gw, nseg - 1) - p * wpp;
-  const int t0 = k * NT / wpp, cnt = (k + 1) * NT / wpp - t0;  // this wave's tiles
-  const int pa = (b * NW) / wpp, plast = min((b * NW + NW - 1) / wpp, npair - 1);
-  const int wi = p / H, h = p - wi * H;
-  const int64_t off = (int64_t)win_slot[wi] * win_stride;
-  const T* kbase = ck + off + (int64_t)h * TKP * 64;
-  const T* vbase = cvt + off + (int64_t)h * 64 * TKP;
-  // tile i of the segment (clamped to its last: loads are never branched around)
-  auto load_kv = [&](int i, Frag<T>(&kf)[4][2], Frag<T>(&vf)[4][2]) {
-    const int kt0 = (t0 + min(i, cnt - 1)) * 64;
+  const int nseg = npair * nsp, nwg = gridDim.x, b = blockIdx.x;
+  const int s0 = (int)((int64_t)b * nseg / nwg), s1 = (int)((int64_t)(b + 1) * nseg / nwg), cnt = s1 - s0;
+  const int pa = s0 / nsp, plast = (s1 - 1) / nsp;
+
+  // tile `tl` (0..XS_T-1) of local segment i: K and V fragments
+  auto load_kv = [&](int i, int tl, Frag<T>(&kf)[4][2], Frag<T>(&vf)[4][2]) {
+    const int gs = s0 + i, p = gs / nsp, k = gs - p * nsp, wi = p / H, h = p - wi * H;
+    const int64_t off = (int64_t)win_slot[wi] * win_stride;
+    const T* kbase = ck + off + (int64_t)h * TKP * 64;
+    const T* vbase = cvt + off + (int64_t)h * 64 * TKP;
+    const int kt0 = (k * XS_T + tl) * 64;
 #pragma unroll
     for (int kt = 0; kt < 4; ++kt) {
       const T* kp = kbase + (int64_t)(kt0 + kt * 16 + r) * 64 + 8 * g;
@@ -1142,11 +936,56 @@ __global__ __launch_bounds__(512, 1) void k_cross_attn_bal(const T* __restrict__
 #pragma unroll
       for (int s = 0; s < 2; ++s) frag_load_stream(vf[dt][s], vbase + (int64_t)(dt * 16 + r) * TKP + kt0 + 32 * s + 8 * g);
   };
-  Frag<T> kf[2][4][2], vf[2][4][2];
-  load_kv(0, kf[0], vf[0]);
-  // the workgroup's pairs' query rows -> LDS (rows past the window's beams repeat its last)
+  // one tile of a segment's online softmax
+  auto tile = [&](const Frag<T>(&kf)[4][2], const Frag<T>(&vf)[4][2], const Frag<T>(&qf)[2], int kt0, float& m,
+                  float& l, float4_t(&acc)[4]) {
+    float4_t sc[4];
 #pragma unroll
-  for (int pass = 0; pass < XB_QPW / 2; ++pass) {
+    for (int kt = 0; kt < 4; ++kt) {
+      sc[kt] = (float4_t){0.f, 0.f, 0.f, 0.f};
+      mfma_step(sc[kt], kf[kt][0], qf[0]);
+      mfma_step(sc[kt], kf[kt][1], qf[1]);
+    }
+    float mx = -INFINITY;
+#pragma unroll
+    for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        if (kt0 + kt * 16 + 4 * g + j >= Tk) sc[kt][j] = -INFINITY;
+        mx = fmaxf(mx, sc[kt][j]);
+      }
+    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    const float mn = fmaxf(m, mx);
+    const float sf = m == -INFINITY ? 0.f : exp2f((m - mn) * XS_LOG2E);
+    m = mn;
+    Frag<T> pf[2];
+    float ps = 0.f;
+#pragma unroll
+    for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float pv = exp2f((sc[kt][j] - m) * XS_LOG2E);
+        ps += pv;
+        pf[kt >> 1].v[(kt & 1) * 4 + j] = from_f32<T>(pv);
+      }
+    ps += __shfl_xor(ps, 16, 64);
+    ps += __shfl_xor(ps, 32, 64);
+    l = l * sf + ps;
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) acc[dt] *= sf;
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) mfma_step(acc[dt], vf[dt][s], pf[s]);
+  };
+
+  Frag<T> kA[4][2], vA[4][2], kB[4][2], vB[4][2];
+  if (wave < cnt) load_kv(wave, 0, kA, vA);
+  // the query rows of the pairs this range touches -> LDS (rows past a window's beams
+  // repeat its last row; K / V stay in flight)
+#pragma unroll
+  for (int pass = 0; pass < XS_QP / 2; ++pass) {
     const int j = 2 * pass + (tid >> 8), t = tid & 255;
     const int pj = min(pa + j, plast), wj = pj / H, hj = pj - wj * H;
     const int qq = min(t >> 4, win_nrows[wj] - 1), c = hj * 64 + (t & 15) * 4, row = win_row0[wj] + qq;
@@ -1166,104 +1005,68 @@ __global__ __launch_bounds__(512, 1) void k_cross_attn_bal(const T* __restrict__
     }
     store4(&qs[j][t >> 4][(t & 15) * 4], qv[0], qv[1], qv[2], qv[3]);
   }
-  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // LDS only: K/V stay in flight
-  Frag<T> qf[2];
-  frag_load(qf[0], &qs[p - pa][r][8 * g]);
-  frag_load(qf[1], &qs[p - pa][r][32 + 8 * g]);
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // LDS only
 
-  float m = -INFINITY, l = 0.f;
-  float4_t acc[4];
+  if (wave < cnt) {
+    for (int i = wave;; i += NW) {
+      const bool more = i + NW < cnt;
+      const int gs = s0 + i, p = gs / nsp, k0 = (gs - p * nsp) * XS_T * 64;
+      Frag<T> qf[2];
+      frag_load(qf[0], &qs[p - pa][r][8 * g]);
+      frag_load(qf[1], &qs[p - pa][r][32 + 8 * g]);
+      float m = -INFINITY, l = 0.f;
+      float4_t acc[4];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) acc[i] = (float4_t){0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-  for (int i = 0; i < TW; ++i) {
-    const int cur = i & 1;
-    if (i + 1 < TW) load_kv(i + 1, kf[cur ^ 1], vf[cur ^ 1]);
-    if (i < cnt) {
-      const int kt0 = (t0 + i) * 64;
-      float4_t sc[4];
-#pragma unroll
-      for (int kt = 0; kt < 4; ++kt) {
-        sc[kt] = (float4_t){0.f, 0.f, 0.f, 0.f};
-        mfma_step(sc[kt], kf[cur][kt][0], qf[0]);
-        mfma_step(sc[kt], kf[cur][kt][1], qf[1]);
+      for (int d = 0; d < 4; ++d) acc[d] = (float4_t){0.f, 0.f, 0.f, 0.f};
+      static_assert(XS_T == 2, "two register sets: tile 0 in A, tile 1 in B");
+      load_kv(i, 1, kB, vB);
+      tile(kA, vA, qf, k0, m, l, acc);
+      if (more) {
+        load_kv(i + NW, 0, kA, vA);  // the wave's next segment streams in meanwhile
+        tile(kB, vB, qf, k0 + 64, m, l, acc);
+      } else {
+        tile(kB, vB, qf, k0 + 64, m, l, acc);
       }
-      float mx = -INFINITY;
+      if (g == 0) {
+        seg_m[i][r] = m;
+        seg_l[i][r] = l;
+      }
 #pragma unroll
-      for (int kt = 0; kt < 4; ++kt)
+      for (int dt = 0; dt < 4; ++dt)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          if (kt0 + kt * 16 + 4 * g + j >= Tk) sc[kt][j] = -INFINITY;
-          mx = fmaxf(mx, sc[kt][j]);
-        }
-      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-      const float mn = fmaxf(m, mx);
-      const float sf = m == -INFINITY ? 0.f : exp2f((m - mn) * LOG2E);
-      m = mn;
-      Frag<T> pf[2];
-      float ps = 0.f;
-#pragma unroll
-      for (int kt = 0; kt < 4; ++kt)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const float pv = exp2f((sc[kt][j] - m) * LOG2E);
-          ps += pv;
-          pf[kt >> 1].v[(kt & 1) * 4 + j] = from_f32<T>(pv);
-        }
-      ps += __shfl_xor(ps, 16, 64);
-      ps += __shfl_xor(ps, 32, 64);
-      l = l * sf + ps;
-#pragma unroll
-      for (int dt = 0; dt < 4; ++dt) acc[dt] *= sf;
-#pragma unroll
-      for (int s = 0; s < 2; ++s)
-#pragma unroll
-        for (int dt = 0; dt < 4; ++dt) mfma_step(acc[dt], vf[cur][dt][s], pf[s]);
+        for (int j = 0; j < 4; ++j) seg_o[i][dt * 16 + 4 * g + j][r] = acc[dt][j];
+      if (!more) break;
     }
   }
-  if (g == 0) {
-    seg_m[wave][r] = m;
-    seg_l[wave][r] = l;
-  }
-#pragma unroll
-  for (int dt = 0; dt < 4; ++dt)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) seg_o[wave][dt * 16 + 4 * g + j][r] = acc[dt][j];
   __syncthreads();
 
   // merge: 256 threads per pair, (row qq, 4 columns dc)
   typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
   const auto rs = __builtin_amdgcn_make_buffer_rsrc(xq.split_rec, 0, 0x7fffffff, 0x00020000);
   const int half = tid >> 8, t = tid & 255, qq = t >> 4, dc = (t & 15) * 4;
-  const int w0 = b * NW;  // first wave (global segment index) of this workgroup
-  auto emit = [&](int pj, float M, float L, float4_t o) {
+  auto emit = [&](int pj, const float4_t& o) {
     const int wj = pj / H, hj = pj - wj * H;
-    if (qq < win_nrows[wj]) {
-      const float inv = 1.f / L;
-      store4(out + (int64_t)(win_row0[wj] + qq) * ldo + hj * 64 + dc, o[0] * inv, o[1] * inv, o[2] * inv, o[3] * inv);
-    }
+    if (qq < win_nrows[wj]) store4(out + (int64_t)(win_row0[wj] + qq) * ldo + hj * 64 + dc, o[0], o[1], o[2], o[3]);
   };
 #pragma unroll
-  for (int pass = 0; pass < XB_QPW / 2; ++pass) {
+  for (int pass = 0; pass < XS_QP / 2; ++pass) {
     const int pj = pa + 2 * pass + half;
     if (pj <= plast) {
-      const int s0 = pj * wpp - w0, s1 = s0 + wpp;  // the pair's segments as local slots
-      if (s0 >= 0 && s1 <= NW) {                     // all here: merge from LDS
-        float M = -INFINITY;
-        for (int s = s0; s < s1; ++s) M = fmaxf(M, seg_m[s][qq]);
-        float L = 0.f;
-        float4_t o = (float4_t){0.f, 0.f, 0.f, 0.f};
-        for (int s = s0; s < s1; ++s) {
-          const float f = seg_m[s][qq] == -INFINITY ? 0.f : exp2f((seg_m[s][qq] - M) * LOG2E);
-          L += f * seg_l[s][qq];
+      const int l0 = pj * nsp - s0, l1 = l0 + nsp;  // the pair's segments as local slots
+      if (l0 >= 0 && l1 <= cnt) {                   // whole here: merge from LDS
+        float mv[XS_NSP], lv[XS_NSP];
+        float4_t ov[XS_NSP];
 #pragma unroll
-          for (int e = 0; e < 4; ++e) o[e] += f * seg_o[s][dc + e][qq];
+        for (int k = 0; k < XS_NSP; ++k) {
+          const int s = min(l0 + k, XS_SMAX - 1);
+          mv[k] = seg_m[s][qq];
+          lv[k] = seg_l[s][qq];
+          ov[k] = (float4_t){seg_o[s][dc][qq], seg_o[s][dc + 1][qq], seg_o[s][dc + 2][qq], seg_o[s][dc + 3][qq]};
         }
-        emit(pj, M, L, o);
-      } else {  // cut: this workgroup's segments of the pair -> records [pair][segment]
-        for (int s = max(s0, 0); s < min(s1, NW); ++s) {
-          const int rb = (pj * wpp + (s - s0)) * XREC * 4;
+        emit(pj, xs_merge(nsp, mv, lv, ov));
+      } else if (qq < win_nrows[pj / H]) {  // cut: this workgroup's segments -> records [pair][segment]
+        for (int s = max(l0, 0); s < min(l1, cnt); ++s) {
+          const int rb = (pj * nsp + (s - l0)) * XREC * 4;
           const float4_t o = (float4_t){seg_o[s][dc][qq], seg_o[s][dc + 1][qq], seg_o[s][dc + 2][qq], seg_o[s][dc + 3][qq]};
           __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, o), rs, rb + (qq * 64 + dc) * 4, 0, 16);
           if (dc == 0) {
@@ -1276,67 +1079,51 @@ __global__ __launch_bounds__(512, 1) void k_cross_attn_bal(const T* __restrict__
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its records
   __syncthreads();
-  // the cut pairs: the first if its segments began in the previous workgroup, the last
-  // if they continue in the next (distinct pairs: a workgroup holds >= 8 / WPP >= 1 whole
-  // segment runs' worth, and a pair spans <= 2 workgroups)
-  const bool cut_first = pa * wpp < w0, cut_last = plast * wpp + wpp > w0 + NW && plast != pa;
+  // the cut pairs: the first if it began before this range, the last if it continues
+  // after it (the same pair when the range lies inside one pair)
+  const bool cut_a = pa * nsp < s0 || pa * nsp + nsp > s1;
+  const bool cut_b = plast != pa && plast * nsp + nsp > s1;
   if (tid == 0) {
-    s_ticket[0] = cut_first ? __hip_atomic_fetch_add(xq.split_cnt + pa, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
-    s_ticket[1] = cut_last ? __hip_atomic_fetch_add(xq.split_cnt + plast, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
+    const int ca = min(s1, pa * nsp + nsp) - s0, cb = s1 - plast * nsp;
+    s_ticket[0] = cut_a && __hip_atomic_fetch_add(xq.split_cnt + pa, ca, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + ca == nsp;
+    s_ticket[1] = cut_b && __hip_atomic_fetch_add(xq.split_cnt + plast, cb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + cb == nsp;
   }
   __syncthreads();
-  const int pj = half ? plast : pa;
-  if (!(half ? (cut_last && s_ticket[1] == 1) : (cut_first && s_ticket[0] == 1))) return;
+  if (!s_ticket[half]) return;
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // no instruction: keeps the loads below the add
+  const int pj = half ? plast : pa;
   if (t == 0) __hip_atomic_store(xq.split_cnt + pj, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  float4_t ov[8];
-  float mv[8], lv[8];
+  if (qq >= win_nrows[pj / H]) return;  // only the window's rows were recorded
+  float mv[XS_NSP], lv[XS_NSP];
+  float4_t ov[XS_NSP];
 #pragma unroll
-  for (int s = 0; s < 8; ++s) {  // every record load issued first (clamped index)
-    const int rb = (pj * wpp + min(s, wpp - 1)) * XREC * 4;
-    ov[s] = __builtin_bit_cast(float4_t, __builtin_amdgcn_raw_buffer_load_b128(rs, rb + (qq * 64 + dc) * 4, 0, 16));
-    mv[s] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, rb + (1024 + qq) * 4, 0, 16));
-    lv[s] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, rb + (1040 + qq) * 4, 0, 16));
+  for (int k = 0; k < XS_NSP; ++k) {  // every record load issued first (clamped index)
+    const int rb = (pj * nsp + min(k, nsp - 1)) * XREC * 4;
+    ov[k] = __builtin_bit_cast(float4_t, __builtin_amdgcn_raw_buffer_load_b128(rs, rb + (qq * 64 + dc) * 4, 0, 16));
+    mv[k] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, rb + (1024 + qq) * 4, 0, 16));
+    lv[k] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, rb + (1040 + qq) * 4, 0, 16));
   }
-  float M = -INFINITY;
-#pragma unroll
-  for (int s = 0; s < 8; ++s)
-    if (s < wpp) M = fmaxf(M, mv[s]);
-  float L = 0.f;
-  float4_t o = (float4_t){0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-  for (int s = 0; s < 8; ++s)
-    if (s < wpp) {
-      const float f = mv[s] == -INFINITY ? 0.f : exp2f((mv[s] - M) * LOG2E);
-      L += f * lv[s];
-#pragma unroll
-      for (int e = 0; e < 4; ++e) o[e] += f * ov[s][e];
-    }
-  emit(pj, M, L, o);
+  emit(pj, xs_merge(nsp, mv, lv, ov));
 }
 
-int cross_attn_bal_enabled() {  // WHISPER_HIP_XBAL=0 keeps one workgroup per pair (A/B)
-  static const int v = [] {
-    const char* e = getenv("WHISPER_HIP_XBAL");
-    return e ? atoi(e) : 1;
-  }();
-  return v;
-}
-
-int cross_attn_split_big() {  // splits at >= 128 (window, head) pairs (WHISPER_HIP_XSPLIT_BIG, A/B)
-  static const int v = [] {
-    const char* e = getenv("WHISPER_HIP_XSPLIT_BIG");
-    return e ? atoi(e) : 1;
-  }();
-  return v;
-}
-
-int cross_attn_split_cap() {
-  static const int cap = [] {
-    const char* e = getenv("WHISPER_HIP_XSPLIT");
-    return e ? atoi(e) : XSPLIT_MAX;
-  }();
-  return cap;
+// Workgroups for nseg segments.  A CU streams its range with 8 waves that each take whole
+// segments, so the slowest wave sets the CU's time: the grid gives every wave the same
+// number of segments k = ceil(nseg / (256 x 8)) (the last workgroup excepted) rather than
+// filling all 256 CUs with uneven waves (20 windows: 200 workgroups of 24 segments, 3 per
+// wave, instead of 256 of 18-19 with 2 or 3 per wave).  k = 1 spreads the segments over
+// up to 256 workgroups (few windows: latency, not bandwidth).  Tuning builds:
+// WHISPER_HIP_XS_K forces k (read per launch).
+int xattn_seg_grid(int npair, int nsp) {
+  const int nseg = npair * nsp;
+  int k = (nseg + 256 * 8 - 1) / (256 * 8);
+  if (const char* e = tune_env("WHISPER_HIP_XS_K")) {
+    const int v = atoi(e);
+    if (v >= 1) k = v;
+  }
+  if (k > XS_SMAX / 8) k = XS_SMAX / 8;
+  int nwg = k == 1 ? (nseg < 256 ? nseg : 256) : (nseg + 8 * k - 1) / (8 * k);
+  if ((nseg + nwg - 1) / nwg > XS_SMAX) nwg = (nseg + XS_SMAX - 1) / XS_SMAX;
+  return nwg;
 }
 
 template <typename T>
@@ -1345,71 +1132,27 @@ void launch_cross_attn(const T* q, int ldq, const T* ck, const T* cv, int Tk, in
                        float* pm, float* pl, T* out, int ldo, int rows, float* qk_out, const int* qk_map, int qk_rows,
                        hipStream_t st, XQPart xq) {
   if (rows <= 0) return;
-  static const bool one = [] {
-    const char* e = getenv("WHISPER_HIP_XATTN1");
-    return !(e && e[0] == '0');
-  }();
-  static const int pf = [] {
-    const char* e = getenv("WHISPER_HIP_XATTN1_PF");
-    return e ? atoi(e) : 1;
-  }();
-  const int ntiles = (Tk + 63) / 64;
-  // many pairs: the balanced kernel (one round, every pair cut into WPP segments)
-  const int npair = nwin * H, wpp = npair > 0 ? std::min(2048 / npair, ntiles) : 0;
-  if (one && cross_attn_bal_enabled() && xq.split_rec && xq.split_cnt && xq.max_rows >= 1 && xq.max_rows <= 16 &&
-      !qk_map && npair >= 256 && wpp >= 3 && wpp <= 8 && npair * wpp <= XREC_CAP) {
-    const int tw = (ntiles + wpp - 1) / wpp, nwg = (npair * wpp + 7) / 8;
-#define XB(QZ_, TW_)                                                                                                 \
-  k_cross_attn_bal<T, QZ_, TW_><<<nwg, 512, 0, st>>>(q, ldq, ck, cv, Tk, H, npair, wpp, win_row0, win_nrows,         \
-                                                     win_slot, win_stride, xq, out, ldo)
-#define XBZ(TW_)                  \
-  switch (xq.part ? xq.z : 0) {   \
-    case 4: XB(4, TW_); break;    \
-    case 8: XB(8, TW_); break;    \
-    case 10: XB(10, TW_); break;  \
-    default: XB(0, TW_); break;   \
-  }
-    if (tw <= 3) XBZ(3)
-    else if (tw == 4) XBZ(4)
-    else if (tw == 5) XBZ(5)
-    else if (tw <= 6) XBZ(6)
-    else XBZ(8)
-#undef XBZ
-#undef XB
-    return;
-  }
-  const int nsp = xq.split_rec && xq.split_cnt ? cross_attn_splits(nwin, H) : 1;
-  const int tpw = ((ntiles + nsp - 1) / nsp + 7) / 8;
-  if (one && xq.max_rows >= 1 && xq.max_rows <= 16 && !qk_map && tpw <= 4) {
-    const dim3 g1(nwin, H, nsp);
-#define XA1(QZ_, TPW_)                                                                                       \
-  if (pf == 2) k_cross_attn1<T, QZ_, TPW_, 2><<<g1, 512, 0, st>>>(q, ldq, ck, cv, Tk, win_row0, win_nrows, win_slot, \
-                                                                  win_stride, xq, out, ldo);                       \
-  else if (pf == 1) k_cross_attn1<T, QZ_, TPW_, 1><<<g1, 512, 0, st>>>(q, ldq, ck, cv, Tk, win_row0, win_nrows,     \
-                                                                       win_slot, win_stride, xq, out, ldo);         \
-  else k_cross_attn1<T, QZ_, TPW_, 0><<<g1, 512, 0, st>>>(q, ldq, ck, cv, Tk, win_row0, win_nrows, win_slot,        \
-                                                          win_stride, xq, out, ldo)
-#define XA1Z(TPW_)                     \
-  switch (xq.part ? xq.z : 0) {        \
-    case 4: XA1(4, TPW_); break;       \
-    case 8: XA1(8, TPW_); break;       \
-    case 10: XA1(10, TPW_); break;     \
-    default: XA1(0, TPW_); break;      \
-  }
-    switch (tpw) {
-      case 1: XA1Z(1) break;
-      case 2: XA1Z(2) break;
-      case 3: XA1Z(3) break;
-      default: XA1Z(4) break;
+  const int ntiles = (Tk + 63) / 64, nsp = ntiles / XS_T;
+  // the decoder step (<= 16 query rows per window, no alignment capture): segments
+  if (xq.max_rows >= 1 && xq.max_rows <= 16 && !qk_map && xq.split_rec && xq.split_cnt && ntiles % XS_T == 0 &&
+      nsp <= XS_NSP && nwin * H <= xq.max_pairs) {
+    const int npair = nwin * H, nwg = xattn_seg_grid(npair, nsp);
+#define XS(QZ_)                                                                                                  \
+  k_xattn_seg<T, QZ_><<<nwg, 512, 0, st>>>(q, ldq, ck, cv, Tk, H, npair, nsp, win_row0, win_nrows, win_slot, \
+                                           win_stride, xq, out, ldo)
+    switch (xq.part ? xq.z : 0) {
+      case 4: XS(4); break;
+      case 8: XS(8); break;
+      case 10: XS(10); break;
+      default: XS(0); break;
     }
-#undef XA1Z
-#undef XA1
+#undef XS
     return;
   }
-  // one 64-key tile per wave, 8 waves per split (3 splits at Tk = 1500: half the
-  // partials of 4-wave splits, -75 us per 20-window beam step)
+  // first passes (prefill, alignment capture): one 64-key tile per wave, 8 waves per
+  // split, partials combined by k_cross_combine
   constexpr int NW = 8;
-  nsplit = ((Tk + 63) / 64 + NW - 1) / NW;
+  nsplit = (ntiles + NW - 1) / NW;
   const dim3 grid(nwin, H, nsplit);
 #define XA(QZ_)                                                                                          \
   k_cross_attn<T, NW, QZ_><<<grid, 64 * NW, 0, st>>>(q, ldq, ck, cv, Tk, H, nsplit, win_row0, win_nrows, win_slot, \
@@ -1593,7 +1336,7 @@ void launch_mel_norm(float* mel, int64_t count, int64_t ld, int n_mels, const un
                                     hipStream_t);                                                                   \
   template void launch_resid_ln<T>(float*, const float*, int, int64_t, const float*, T*, const float*, const float*, \
                                    int, int, float, hipStream_t);                                                   \
-  template void launch_self_attn_qkv<T>(const float*, int, int64_t, const float*, int, T*, T*, const int*, const int*, \
+  template int launch_self_attn_qkv<T>(const float*, int, int64_t, const float*, int, T*, T*, const int*, const int*, \
                                         const int*, const int*, int, int, int, int, T*, int, int, hipStream_t);     \
   template void launch_reduce_store<T>(const float*, int, int64_t, const float*, T*, int, int, int, int, hipStream_t); \
   template void launch_attn_enc<T>(const T*, int, int, int, int, int, int64_t, const T*, int, T*, int64_t,         \

@@ -58,7 +58,7 @@ template <typename T>
 int launch_proj_partial(const GemmArgs& a, int max_z, hipStream_t st, int* z_out, hipEvent_t ev0, hipEvent_t ev1) {
   static Table<T> tab;
   static const bool off = [] {
-    const char* e = getenv("WHISPER_HIP_PROJ");
+    const char* e = tune_env("WHISPER_HIP_PROJ");
     return e && e[0] == '0';
   }();
   if (off || a.M < 1 || a.M > 112 || a.K % 32 || a.N % 16 || a.x_group_rows < a.M) return -1;
@@ -66,7 +66,7 @@ int launch_proj_partial(const GemmArgs& a, int max_z, hipStream_t st, int* z_out
   // tuning override: WHISPER_HIP_PROJ_FORCE="N:K:cfg,..." pins the CFGS entry per shape
   static const std::vector<std::array<int, 3>> force = [] {
     std::vector<std::array<int, 3>> v;
-    if (const char* e = getenv("WHISPER_HIP_PROJ_FORCE")) {
+    if (const char* e = tune_env("WHISPER_HIP_PROJ_FORCE")) {
       int n, k, c, off = 0, used = 0;
       while (sscanf(e + off, "%d:%d:%d%n", &n, &k, &c, &used) == 3) {
         v.push_back({n, k, c});

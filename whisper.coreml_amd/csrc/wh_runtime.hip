@@ -50,7 +50,7 @@ constexpr int NSPLIT = 8;         // cross-attention key splits (1500 / 8 = 188 
 // encoder windows per pass (WHISPER_HIP_ENC_CHUNK overrides; activations scale with it)
 static int enc_chunk() {
   static const int v = [] {
-    const char* e = getenv("WHISPER_HIP_ENC_CHUNK");
+    const char* e = tune_env("WHISPER_HIP_ENC_CHUNK");
     const int c = e ? atoi(e) : 16;
     return c >= 1 && c <= 64 ? c : 16;
   }();
@@ -96,6 +96,7 @@ struct Timer {
 }  // namespace
 
 struct wh_ctx {
+  virtual std::string step_kernels(int n_win, int group) const = 0;
   virtual ~wh_ctx() {}
   virtual int load(const std::string& name, const float* data, const int64_t* shape, int ndim) = 0;
   virtual int finalize() = 0;
@@ -186,7 +187,7 @@ struct Ctx : public wh_ctx {
   static constexpr int P1_SLABS = 2048;  // k_proj1 split-K slabs: zs x 16-column tiles <= 16 x 80 at n = 1280
   float* p1_slab = nullptr;  // k_proj1 in-launch split-K slabs [zs][N/16][256]
   int* p1_cnt = nullptr;     // and arrival counters [4n/16] (zero between launches)
-  float* xs_rec = nullptr;   // step cross-attention key-split records (<= XREC_CAP x XREC)
+  float* xs_rec = nullptr;   // step cross-attention segment records [pair][XS_NSP][XREC]
   int* xs_cnt = nullptr;     // and (window, head) arrival counters
 
   // the step cross-attention's query / split arguments
@@ -195,6 +196,7 @@ struct Ctx : public wh_ctx {
     xq.max_rows = rows_per_window;
     xq.split_rec = xs_rec;
     xq.split_cnt = xs_cnt;
+    xq.max_pairs = Wcap * nh;
     return xq;
   }
   int* qk_map;  // [Ld][nh]
@@ -329,7 +331,7 @@ struct Ctx : public wh_ctx {
     addA(64);
     addA(64);
     addA((size_t)P1_SLABS * 256 * 4); addA((size_t)(4 * n / 16) * 4);  // k_proj1 split-K slabs + counters
-    addA((size_t)XREC_CAP * XREC * 4); addA((size_t)Wcap * nh * 4);           // cross-attention split records
+    addA((size_t)Wcap * nh * XS_NSP * XREC * 4); addA((size_t)Wcap * nh * 4);  // cross-attention segment records
     HIPCHK(hipMalloc(&abase, ab));
     HIPCHK(hipMemset(abase, 0, ab));
     aa.base = (char*)abase;
@@ -363,7 +365,7 @@ struct Ctx : public wh_ctx {
     S.lpart = fa((size_t)Wcap * Gcap * LP_SLICES * LP_REC);
     S.seed = (unsigned long long*)aa.take(64);
     p1_slab = fa((size_t)P1_SLABS * 256); p1_cnt = ia(4 * n / 16);  // zeroed with the arena
-    xs_rec = fa((size_t)XREC_CAP * XREC); xs_cnt = ia((size_t)Wcap * nh);
+    xs_rec = fa((size_t)Wcap * nh * XS_NSP * XREC); xs_cnt = ia((size_t)Wcap * nh);
     if (!S.seed || !S.cand_idx || !p1_cnt || !xs_cnt) return fail(-3, "activation arena overflow");
     S.nw = Wcap; S.G = 1; S.ctx = CTX; S.hctx = HCTX; S.maxc = 16;
     HIPCHK(hipMalloc(&d_gmax, 64));
@@ -778,8 +780,9 @@ struct Ctx : public wh_ctx {
       if (skinny) {
         int ks = 0;
         TRY(partial(xn_d, n, e.wqkv, R, 3 * n, n, &ks));
-        launch_self_attn_qkv<T>(part, ks, (int64_t)R * 3 * n, e.bqkv, n, kc[l], vc[l], rw, rs, rp, S.anc, ancG, Gcap,
-                                nh, CTX, att_d, n, R, st);
+        if (launch_self_attn_qkv<T>(part, ks, (int64_t)R * 3 * n, e.bqkv, n, kc[l], vc[l], rw, rs, rp, S.anc, ancG,
+                                    Gcap, nh, CTX, att_d, n, R, st))
+          return fail(-20, "self-attention rows are not a whole number of beam groups");
       } else {
         g = GemmArgs();
         g.out = q_d; g.ldo = n; g.hs_state = n; g.hs_heads = nh;
@@ -823,7 +826,7 @@ struct Ctx : public wh_ctx {
   // WHISPER_HIP_P1=0 keeps the split-K path (A/B).
   static bool p1_enabled() {
     static const bool on = [] {
-      const char* e = getenv("WHISPER_HIP_P1");
+      const char* e = tune_env("WHISPER_HIP_P1");
       return !(e && e[0] == '0');
     }();
     return on;
@@ -883,6 +886,9 @@ struct Ctx : public wh_ctx {
   }
 
   bool p1_active(int R) const { return p1_enabled() && proj1_supported(R, ns); }
+  std::string step_kernels(int n_win, int group) const override {
+    return std::string("proj=") + (p1_active(n_win * group) ? "k_proj1" : "k_proj") + ",xattn=k_xattn_seg";
+  }
 
   int dec_layers_p1(int R, const int* rw, const int* rs, const int* rp, int ancG, int nwin, const int* wr0,
                     const int* wnr, const int* wsl) {
@@ -1012,6 +1018,10 @@ struct Ctx : public wh_ctx {
   int begin_batch(int n_win, int G, const int* init, const int* n_init, int max_init, const int* sot_index,
                   int no_speech, const int* slots = nullptr) {
     if (!finalized) return fail(-9, "weights not finalized");
+    // no usable batch until this one is fully set up: a failure below leaves neither the
+    // device loop nor the per-step ABI (wh_step / wh_reorder_kv) a half-written batch
+    cur_nwin = 0;
+    step_api = false;
     if (n_win < 1 || n_win > Wcap) return fail(-11, "n_win out of range");
     if (G < 1 || G > Gcap) return fail(-11, "group exceeds context max_group");
     win_slots.resize(n_win);
@@ -1211,14 +1221,14 @@ struct Ctx : public wh_ctx {
 
   // WHISPER_HIP_XQ=0 keeps the separate cross-query reduce (A/B switch)
   const bool xq_fused = [] {
-    const char* e = getenv("WHISPER_HIP_XQ");
+    const char* e = tune_env("WHISPER_HIP_XQ");
     return !(e && e[0] == '0');
   }();
 
   // WHISPER_HIP_EAGER=1 launches the step kernels directly instead of replaying the
   // captured graph (same kernels; used under profilers that do not follow graphs)
   bool eager() const {
-    const char* e = getenv("WHISPER_HIP_EAGER");
+    const char* e = tune_env("WHISPER_HIP_EAGER");
     return e && e[0] == '1';
   }
 
@@ -1235,7 +1245,7 @@ struct Ctx : public wh_ctx {
     hipEventRecord(tm.a, st);
     int steps = 0, done = 0;
     static const int chunk = [] {  // WHISPER_HIP_POLL_CHUNK: steps per done-flag poll (A/B)
-      const char* e = getenv("WHISPER_HIP_POLL_CHUNK");
+      const char* e = tune_env("WHISPER_HIP_POLL_CHUNK");
       const int v = e ? atoi(e) : 8;
       return v < 1 ? 1 : v;
     }();
@@ -1540,7 +1550,7 @@ struct Ctx : public wh_ctx {
       // per-launch time of one decoder-step kernel at the current batch, over all
       // layers (so weights / cross-KV stream from HBM as in the step, not from cache):
       // 2 = the six split-K projection GEMVs of each layer (k_gemv_x, EPI_PARTIAL),
-      // 3 = the step's cross-attention (k_cross_attn1)
+      // 3 = the step's cross-attention (k_xattn_seg)
       // 5 / 6 = 2 / 3 on layer 0 only, repeated (operands Infinity-Cache warm)
       if (cur_nwin < 1) return fail(-16, "no decode batch");
       const bool warm = what >= 5;
@@ -1558,7 +1568,7 @@ struct Ctx : public wh_ctx {
           } else {
             const T* ck = ckv + (size_t)(2 * l) * Wcap * TKP * n;
             const T* cv = ckv + (size_t)(2 * l + 1) * Wcap * TKP * n;
-            const XQPart xq = step_xq(cur_G);  // the step's kernel (k_cross_attn1), query from q_d
+            const XQPart xq = step_xq(cur_G);  // the step's kernel (k_xattn_seg), query from q_d
             launch_cross_attn<T>(q_d, n, ck, cv, 1500, nh, NSPLIT, cur_nwin, st_win_row0, st_win_nrows, st_win_slot,
                                  (int64_t)TKP * n, po, pm, pl, att_d, n, R, nullptr, nullptr, 0, st, xq);
             ++launches;
@@ -1759,6 +1769,14 @@ int wh_stats(wh_ctx* ctx, double* out, int n) {
   if (!ctx || !out) return fail(-1, "null argument");
   for (int i = 0; i < n && i < 8; ++i) out[i] = ctx->stats[i];
   return 0;
+}
+int wh_step_kernels(wh_ctx* ctx, int n_win, int group, char* buf, int cap) {
+  if (!ctx || !buf || cap < 1) return fail(-1, "bad arguments");
+  const std::string d = ctx->step_kernels(n_win, group);
+  const int n = std::min<int>((int)d.size(), cap - 1);
+  memcpy(buf, d.data(), n);
+  buf[n] = 0;
+  return n;
 }
 int wh_sync(wh_ctx* ctx) {
   if (!ctx) return fail(-1, "null context");

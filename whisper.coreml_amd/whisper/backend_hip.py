@@ -80,6 +80,7 @@ _EXPORTS = {
     "wh_stats": (c_int, [c_void_p, POINTER(c_double), c_int]),
     "wh_sync": (c_int, [c_void_p]),
     "wh_time_stage": (c_int, [c_void_p, c_int, c_int, POINTER(c_double)]),
+    "wh_step_kernels": (c_int, [c_void_p, c_int, c_int, ctypes.c_char_p, c_int]),
     "wh_token_ms": (c_int, [c_void_p, c_void_p, c_int, POINTER(c_int), c_int]),
     "wh_flac_info": (c_int, [c_void_p, c_int64, POINTER(c_int), POINTER(c_int), POINTER(c_int), POINTER(c_int64)]),
     "wh_flac_decode": (c_int, [c_void_p, c_int64, c_void_p, c_int64, POINTER(c_int64)]),
@@ -397,6 +398,14 @@ class HipContext:
         out = np.zeros(max(n.value, 1), np.float32)
         self._check(self.lib.wh_token_ms(self.h, _ptr(out), n.value, ctypes.byref(n), int(reset)), "wh_token_ms")
         return out[:n.value]
+
+    def step_kernels(self, n_win: int, group: int) -> dict:
+        """The kernels the decoder step runs for this batch shape (wh_step_kernels):
+        {"proj": ..., "xattn": ...}."""
+        buf = ctypes.create_string_buffer(256)
+        n = self.lib.wh_step_kernels(self.h, n_win, group, buf, 256)
+        self._check(0 if n >= 0 else n, "wh_step_kernels")
+        return dict(kv.split("=", 1) for kv in buf.value.decode().split(","))
 
     def time_stage(self, what: int, iters: int) -> float:
         ms = c_double()

@@ -105,12 +105,15 @@ class DecodingTask:
         return list(v)
 
     def _initial_tokens(self, prompt) -> Tuple[int, ...]:
-        """decoding.py:614-640."""
+        """decoding.py:614-640, Python slice semantics included: with the default
+        sample_len max_prefix_len is 0 and [-0:] keeps the whole prefix; a negative
+        max_prefix_len (sample_len > n_ctx // 2) drops the FIRST -max_prefix_len tokens."""
         toks = list(self.sot_sequence)
         if self.options.prefix:
             pre = self._text_ids(self.options.prefix)
             if self.sample_len is not None:
-                pre = pre[-(self.n_ctx // 2 - self.sample_len):] if self.n_ctx // 2 - self.sample_len > 0 else []
+                max_prefix_len = self.n_ctx // 2 - self.sample_len
+                pre = pre[-max_prefix_len:]
             toks = toks + pre
         if prompt:
             p = self._text_ids(prompt)
@@ -221,6 +224,9 @@ def decode(model: "Whisper", mel, options: DecodingOptions = DecodingOptions(), 
         mel = mel[None]
     if kwargs:
         options = replace(options, **kwargs)
+    if not options.fp16 and model.dtype != "fp32":
+        # decoding.py:745-752 would compute in fp32; the context's precision is fixed at load
+        raise ValueError("DecodingOptions(fp16=False) needs a context loaded with dtype='fp32'")
     n = mel.shape[0]
     if n > model.ctx.max_windows:
         res = []

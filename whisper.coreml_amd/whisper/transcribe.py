@@ -119,6 +119,18 @@ def _split_segments(tokenizer, result: DecodingResult, seek: int, time_offset: f
     return segs, seek, single_end
 
 
+def _check_fp16(model: "Whisper", fp16: bool):
+    """transcribe.py:131-140 picks the compute dtype from ``fp16``; here the precision is
+    fixed when the context is created (``load_model(..., dtype=)``).  fp16=True on an
+    fp32 context falls back to fp32 with the reference's warning; fp16=False on an fp16
+    context cannot be honoured and raises instead of silently computing in fp16."""
+    if fp16 and model.dtype == "fp32":
+        warnings.warn("FP16 requested but the model was loaded with dtype='fp32'; using FP32 instead")
+    elif not fp16 and model.dtype != "fp32":
+        raise ValueError("fp16=False needs a context loaded with dtype='fp32' "
+                         "(load_model(..., dtype='fp32')); this one computes in fp16")
+
+
 def _clear_empty(tokenizer, segs: List[dict]):
     """transcribe.py:494-499 (after word timestamps)."""
     for s in segs:
@@ -142,9 +154,7 @@ def transcribe(model: "Whisper", audio: Union[str, np.ndarray], *, verbose: Opti
     "batched") and ``mel_max_reduce`` (callable local max -> global max, used when
     one file is sharded over GPUs: the log-mel floor is a whole-file max,
     audio.py:155, so ranks all-reduce it before normalizing)."""
-    if decode_options.get("fp16", True) is False and model.dtype != "fp32":
-        pass  # the compute precision is fixed when the model is loaded (dtype=...)
-    decode_options.pop("fp16", None)
+    _check_fp16(model, decode_options.pop("fp16", True))
     ctx = model.ctx
     n_mels = model.dims.n_mels
     if _mel_prepared is not None:
