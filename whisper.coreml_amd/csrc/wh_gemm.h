@@ -54,6 +54,14 @@ struct GemmArgs {
   float* p1_slab = nullptr;
   int* p1_cnt = nullptr;
   int p1_slabs = 0;  // slab capacity (1 KB slabs) of p1_slab
+  // k_proj1 deferred residual (wh_proj.h): a residual projection launched with p1_defer
+  // only stores its two K-half slabs; the next LayerNorm prologue (res_slab != null)
+  // forms x_new = xf32 + ((slab0 + slab1) + res_bias), normalises it, and the workgroup
+  // (0, 0) writes x_new to x_out (another buffer: the other workgroups still read xf32)
+  int p1_defer = 0;
+  const float* res_slab = nullptr;
+  const float* res_bias = nullptr;
+  float* x_out = nullptr;
 };
 
 template <typename T, int EPI>

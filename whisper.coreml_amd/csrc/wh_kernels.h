@@ -43,15 +43,11 @@ struct XQPart {
   int max_pairs = 0;
 };
 constexpr int XREC = 16 * 64 + 32;  // floats per segment record: O[16][64], m[16], l[16]
-// step cross-attention segments (k_xattn_seg): XS_T key tiles of 64 per segment, at
-// most XS_NSP segments per (window, head) pair (Tk <= XS_NSP * XS_T * 64 = 1536), at
-// most XS_SMAX segments per workgroup, at most XS_QP pairs per workgroup's range
-constexpr int XS_T = 2;
-constexpr int XS_NSP = 12;
-constexpr int XS_SMAX = 24;
+// step cross-attention (k_xattn_seg): one softmax partial per 64-key tile, at most
+// XS_NSP tiles per (window, head) pair (Tk <= 1536), at most XS_QP pairs per workgroup
+constexpr int XS_NSP = 24;
 constexpr int XS_QP = 4;
-static_assert((XS_SMAX + XS_NSP - 1) / XS_NSP + 1 <= XS_QP, "pairs per workgroup range");
-int xattn_seg_grid(int npair, int nsp);
+int xattn_seg_grid(int npair, int nsp, int smax);
 inline bool cross_attn_q_slabs(int z) { return z == 4 || z == 8 || z == 10; }
 template <typename T>
 void launch_cross_attn(const T* q, int ldq, const T* ck, const T* cv, int Tk, int H, int nsplit, int nwin,

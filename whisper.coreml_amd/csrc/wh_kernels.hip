@@ -859,57 +859,71 @@ __global__ __launch_bounds__(64) void k_cross_combine(const float* __restrict__ 
 // Decoder-step cross-attention (decoder.py:74-91 for the step's query rows: <= 16 rows
 // per window, the beams), batch-invariant and balanced over the chip.
 //
-// Numerics are fixed per (window, head) pair, whatever the batch: the pair's 64-key
-// tiles form nsp = ceil(Tk / 64) / XS_T segments of XS_T tiles; a segment's online
-// softmax runs over its tiles in order, and the pair's nsp (m, l, O) records are merged
-// in segment order by xs_merge.  How many windows share the launch changes only which
-// workgroup computes a segment and where it is merged, never an arithmetic operation,
-// so a window's output is bit-identical in any batch.
+// Numerics are fixed per (window, head) pair, whatever the batch: every 64-key tile of
+// the pair gives one softmax partial (m = the tile's max score, l = sum exp(s - m),
+// O = sum exp(s - m) v), and the pair's nsp = ceil(Tk / 64) partials are merged in tile
+// order by the flat merge of xs_merge (M = max m, then L and O accumulated over the
+// tiles in order).  How many windows share the launch changes only which workgroup
+// computes a tile and where the pair is merged, never an arithmetic operation, so a
+// window's output is bit-identical in any batch.
 //
-// Work distribution (speed only): the segments of all pairs, in (pair, segment) order,
-// are dealt in contiguous ranges to nwg workgroups (<= 256: one per CU, each range
-// <= XS_SMAX segments); the workgroup's 8 waves take its segments round-robin, each
-// with the next tile's K and V in flight (the last segment of a wave is peeled, so no
-// load is clamped or wasted).  A pair whose segments are all in the workgroup merges
-// from LDS.  A pair cut between workgroups has this workgroup's records stored
-// write-through (sc1) at [pair][segment], drained by every storing wave, and counted on
-// the pair's arrival counter (relaxed agent atomic, + the segments contributed); the
-// workgroup that completes the count re-arms it and merges all records with sc1 loads
-// (cdna_hip_programming.md §6 Guideline 16 R1, MI355X_MICROARCH.md "Valid forms").
+// Work distribution (speed only): the tiles of all pairs, in (pair, tile) order, are
+// dealt in contiguous ranges to nwg <= 256 workgroups; the workgroup's 8 waves take its
+// tiles round-robin, the next tile's K and V in flight while one is computed (no tile
+// depends on another, the last one is peeled: no load is clamped or wasted).  A pair
+// whose tiles are all in the workgroup merges from LDS.  A pair cut between workgroups
+// has this workgroup's partials stored write-through (sc1) at [pair][tile] (the window's
+// rows only), drained by every storing wave, and counted on the pair's arrival counter
+// (relaxed agent atomic, + the tiles contributed); the workgroup that completes the
+// count re-arms it and merges every partial with sc1 loads (cdna_hip_programming.md §6
+// Guideline 16 R1, MI355X_MICROARCH.md "Valid forms").  RR: rows kept per partial in LDS
+// (8 when the beams are <= 8, else 16).
 // K: [slot][head][TKP][64]; V transposed [slot][head][64][TKP] with the 32-key
 // permutation, so both MFMA operands load straight from HBM into fragments.
 constexpr float XS_LOG2E = 1.4426950408889634f;
 
-// the pair merge, shared by the LDS and the record path (identical operations)
-WH_DEV float4_t xs_merge(int n, const float (&mv)[XS_NSP], const float (&lv)[XS_NSP], const float4_t (&ov)[XS_NSP]) {
+template <int RR>
+struct XsShape {
+  static constexpr int SMAX = RR == 8 ? 48 : 32;  // tiles per workgroup (LDS partials)
+};
+
+// the pair merge shared by the LDS and the record path: `get(k, m, l, o)` fetches tile
+// k's partial; every fetch is issued before the first use (one round trip on the record
+// path), then M = max m, and L, O accumulate over the tiles in order
+template <typename Get>
+WH_DEV float4_t xs_merge(int n, Get get) {
+  float mv[XS_NSP], lv[XS_NSP];
+  float4_t ov[XS_NSP];
+#pragma unroll
+  for (int k = 0; k < XS_NSP; ++k) get(k < n ? k : n - 1, mv[k], lv[k], ov[k]);
   float M = -INFINITY;
 #pragma unroll
   for (int k = 0; k < XS_NSP; ++k)
     if (k < n) M = fmaxf(M, mv[k]);
   float L = 0.f;
-  float4_t o = (float4_t){0.f, 0.f, 0.f, 0.f};
+  float4_t acc = (float4_t){0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int k = 0; k < XS_NSP; ++k)
     if (k < n) {
       const float f = mv[k] == -INFINITY ? 0.f : exp2f((mv[k] - M) * XS_LOG2E);
       L = __builtin_fmaf(f, lv[k], L);
 #pragma unroll
-      for (int e = 0; e < 4; ++e) o[e] = __builtin_fmaf(f, ov[k][e], o[e]);
+      for (int e = 0; e < 4; ++e) acc[e] = __builtin_fmaf(f, ov[k][e], acc[e]);
     }
   const float inv = 1.f / L;
-  return o * inv;
+  return acc * inv;
 }
 
-template <typename T, int QZ>
+template <typename T, int QZ, int RR>
 __global__ __launch_bounds__(512, 1) void k_xattn_seg(const T* __restrict__ q, int ldq, const T* ck, const T* cvt, int Tk,
                                                      int H, int npair, int nsp, const int* __restrict__ win_row0,
                                                      const int* __restrict__ win_nrows,
                                                      const int* __restrict__ win_slot, int64_t win_stride, XQPart xq,
                                                      T* __restrict__ out, int ldo) {
-  constexpr int NW = 8;
+  constexpr int NW = 8, SMAX = XsShape<RR>::SMAX, PPASS = 512 / (RR * 16);  // pairs merged per pass
   constexpr bool QP = QZ > 0;
-  __shared__ float seg_m[XS_SMAX][16], seg_l[XS_SMAX][16];
-  __shared__ float seg_o[XS_SMAX][64][17];
+  __shared__ float seg_m[SMAX][RR], seg_l[SMAX][RR];
+  __shared__ float seg_o[SMAX][64][RR + 1];
   __shared__ __attribute__((aligned(16))) T qs[XS_QP][16][72];
   __shared__ int s_ticket[2];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -918,13 +932,13 @@ __global__ __launch_bounds__(512, 1) void k_xattn_seg(const T* __restrict__ q, i
   const int s0 = (int)((int64_t)b * nseg / nwg), s1 = (int)((int64_t)(b + 1) * nseg / nwg), cnt = s1 - s0;
   const int pa = s0 / nsp, plast = (s1 - 1) / nsp;
 
-  // tile `tl` (0..XS_T-1) of local segment i: K and V fragments
-  auto load_kv = [&](int i, int tl, Frag<T>(&kf)[4][2], Frag<T>(&vf)[4][2]) {
+  // local tile i: K and V fragments
+  auto load_kv = [&](int i, Frag<T>(&kf)[4][2], Frag<T>(&vf)[4][2]) {
     const int gs = s0 + i, p = gs / nsp, k = gs - p * nsp, wi = p / H, h = p - wi * H;
     const int64_t off = (int64_t)win_slot[wi] * win_stride;
     const T* kbase = ck + off + (int64_t)h * TKP * 64;
     const T* vbase = cvt + off + (int64_t)h * 64 * TKP;
-    const int kt0 = (k * XS_T + tl) * 64;
+    const int kt0 = k * 64;
 #pragma unroll
     for (int kt = 0; kt < 4; ++kt) {
       const T* kp = kbase + (int64_t)(kt0 + kt * 16 + r) * 64 + 8 * g;
@@ -936,9 +950,12 @@ __global__ __launch_bounds__(512, 1) void k_xattn_seg(const T* __restrict__ q, i
 #pragma unroll
       for (int s = 0; s < 2; ++s) frag_load_stream(vf[dt][s], vbase + (int64_t)(dt * 16 + r) * TKP + kt0 + 32 * s + 8 * g);
   };
-  // one tile of a segment's online softmax
-  auto tile = [&](const Frag<T>(&kf)[4][2], const Frag<T>(&vf)[4][2], const Frag<T>(&qf)[2], int kt0, float& m,
-                  float& l, float4_t(&acc)[4]) {
+  // local tile i's softmax partial -> LDS slot i
+  auto tile = [&](const Frag<T>(&kf)[4][2], const Frag<T>(&vf)[4][2], int i) {
+    const int gs = s0 + i, p = gs / nsp, kt0 = (gs - p * nsp) * 64;
+    Frag<T> qf[2];
+    frag_load(qf[0], &qs[p - pa][r][8 * g]);
+    frag_load(qf[1], &qs[p - pa][r][32 + 8 * g]);
     float4_t sc[4];
 #pragma unroll
     for (int kt = 0; kt < 4; ++kt) {
@@ -956,32 +973,39 @@ __global__ __launch_bounds__(512, 1) void k_xattn_seg(const T* __restrict__ q, i
       }
     mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
     mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-    const float mn = fmaxf(m, mx);
-    const float sf = m == -INFINITY ? 0.f : exp2f((m - mn) * XS_LOG2E);
-    m = mn;
     Frag<T> pf[2];
     float ps = 0.f;
 #pragma unroll
     for (int kt = 0; kt < 4; ++kt)
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        const float pv = exp2f((sc[kt][j] - m) * XS_LOG2E);
+        const float pv = exp2f((sc[kt][j] - mx) * XS_LOG2E);
         ps += pv;
         pf[kt >> 1].v[(kt & 1) * 4 + j] = from_f32<T>(pv);
       }
     ps += __shfl_xor(ps, 16, 64);
     ps += __shfl_xor(ps, 32, 64);
-    l = l * sf + ps;
+    float4_t acc[4];
 #pragma unroll
-    for (int dt = 0; dt < 4; ++dt) acc[dt] *= sf;
+    for (int dt = 0; dt < 4; ++dt) acc[dt] = (float4_t){0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int s = 0; s < 2; ++s)
 #pragma unroll
       for (int dt = 0; dt < 4; ++dt) mfma_step(acc[dt], vf[dt][s], pf[s]);
+    if (r < RR) {
+      if (g == 0) {
+        seg_m[i][r] = mx;
+        seg_l[i][r] = ps;
+      }
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) seg_o[i][dt * 16 + 4 * g + j][r] = acc[dt][j];
+    }
   };
 
   Frag<T> kA[4][2], vA[4][2], kB[4][2], vB[4][2];
-  if (wave < cnt) load_kv(wave, 0, kA, vA);
+  if (wave < cnt) load_kv(wave, kA, vA);
   // the query rows of the pairs this range touches -> LDS (rows past a window's beams
   // repeat its last row; K / V stay in flight)
 #pragma unroll
@@ -1008,63 +1032,45 @@ __global__ __launch_bounds__(512, 1) void k_xattn_seg(const T* __restrict__ q, i
   asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // LDS only
 
   if (wave < cnt) {
-    for (int i = wave;; i += NW) {
-      const bool more = i + NW < cnt;
-      const int gs = s0 + i, p = gs / nsp, k0 = (gs - p * nsp) * XS_T * 64;
-      Frag<T> qf[2];
-      frag_load(qf[0], &qs[p - pa][r][8 * g]);
-      frag_load(qf[1], &qs[p - pa][r][32 + 8 * g]);
-      float m = -INFINITY, l = 0.f;
-      float4_t acc[4];
-#pragma unroll
-      for (int d = 0; d < 4; ++d) acc[d] = (float4_t){0.f, 0.f, 0.f, 0.f};
-      static_assert(XS_T == 2, "two register sets: tile 0 in A, tile 1 in B");
-      load_kv(i, 1, kB, vB);
-      tile(kA, vA, qf, k0, m, l, acc);
-      if (more) {
-        load_kv(i + NW, 0, kA, vA);  // the wave's next segment streams in meanwhile
-        tile(kB, vB, qf, k0 + 64, m, l, acc);
-      } else {
-        tile(kB, vB, qf, k0 + 64, m, l, acc);
-      }
-      if (g == 0) {
-        seg_m[i][r] = m;
-        seg_l[i][r] = l;
-      }
-#pragma unroll
-      for (int dt = 0; dt < 4; ++dt)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) seg_o[i][dt * 16 + 4 * g + j][r] = acc[dt][j];
-      if (!more) break;
+    int i = wave;
+    // two tiles per iteration, the next one always in flight (unconditional loads)
+    for (; i + 2 * NW < cnt; i += 2 * NW) {
+      load_kv(i + NW, kB, vB);
+      tile(kA, vA, i);
+      load_kv(i + 2 * NW, kA, vA);
+      tile(kB, vB, i + NW);
+    }
+    if (i + NW < cnt) {
+      load_kv(i + NW, kB, vB);
+      tile(kA, vA, i);
+      tile(kB, vB, i + NW);
+    } else {
+      tile(kA, vA, i);
     }
   }
   __syncthreads();
 
-  // merge: 256 threads per pair, (row qq, 4 columns dc)
+  // merge: RR * 16 threads per pair, (row qq, 4 columns dc)
   typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
   const auto rs = __builtin_amdgcn_make_buffer_rsrc(xq.split_rec, 0, 0x7fffffff, 0x00020000);
-  const int half = tid >> 8, t = tid & 255, qq = t >> 4, dc = (t & 15) * 4;
+  const int part = tid / (RR * 16), t = tid - part * (RR * 16), qq = t >> 4, dc = (t & 15) * 4;
   auto emit = [&](int pj, const float4_t& o) {
     const int wj = pj / H, hj = pj - wj * H;
-    if (qq < win_nrows[wj]) store4(out + (int64_t)(win_row0[wj] + qq) * ldo + hj * 64 + dc, o[0], o[1], o[2], o[3]);
+    store4(out + (int64_t)(win_row0[wj] + qq) * ldo + hj * 64 + dc, o[0], o[1], o[2], o[3]);
   };
 #pragma unroll
-  for (int pass = 0; pass < XS_QP / 2; ++pass) {
-    const int pj = pa + 2 * pass + half;
-    if (pj <= plast) {
-      const int l0 = pj * nsp - s0, l1 = l0 + nsp;  // the pair's segments as local slots
+  for (int pass = 0; pass < (XS_QP + PPASS - 1) / PPASS; ++pass) {
+    const int pj = pa + pass * PPASS + part;
+    if (pj <= plast && qq < win_nrows[pj / H]) {
+      const int l0 = pj * nsp - s0, l1 = l0 + nsp;  // the pair's tiles as local slots
       if (l0 >= 0 && l1 <= cnt) {                   // whole here: merge from LDS
-        float mv[XS_NSP], lv[XS_NSP];
-        float4_t ov[XS_NSP];
-#pragma unroll
-        for (int k = 0; k < XS_NSP; ++k) {
-          const int s = min(l0 + k, XS_SMAX - 1);
-          mv[k] = seg_m[s][qq];
-          lv[k] = seg_l[s][qq];
-          ov[k] = (float4_t){seg_o[s][dc][qq], seg_o[s][dc + 1][qq], seg_o[s][dc + 2][qq], seg_o[s][dc + 3][qq]};
-        }
-        emit(pj, xs_merge(nsp, mv, lv, ov));
-      } else if (qq < win_nrows[pj / H]) {  // cut: this workgroup's segments -> records [pair][segment]
+        emit(pj, xs_merge(nsp, [&](int k, float& m, float& l, float4_t& o) {
+               m = seg_m[l0 + k][qq];
+               l = seg_l[l0 + k][qq];
+               o = (float4_t){seg_o[l0 + k][dc][qq], seg_o[l0 + k][dc + 1][qq], seg_o[l0 + k][dc + 2][qq],
+                              seg_o[l0 + k][dc + 3][qq]};
+             }));
+      } else {  // cut: this workgroup's partials of the pair -> records [pair][tile]
         for (int s = max(l0, 0); s < min(l1, cnt); ++s) {
           const int rb = (pj * nsp + (s - l0)) * XREC * 4;
           const float4_t o = (float4_t){seg_o[s][dc][qq], seg_o[s][dc + 1][qq], seg_o[s][dc + 2][qq], seg_o[s][dc + 3][qq]};
@@ -1089,40 +1095,41 @@ __global__ __launch_bounds__(512, 1) void k_xattn_seg(const T* __restrict__ q, i
     s_ticket[1] = cut_b && __hip_atomic_fetch_add(xq.split_cnt + plast, cb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + cb == nsp;
   }
   __syncthreads();
-  if (!s_ticket[half]) return;
+  if (part > 1 || !s_ticket[part]) return;
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // no instruction: keeps the loads below the add
-  const int pj = half ? plast : pa;
+  const int pj = part ? plast : pa;
   if (t == 0) __hip_atomic_store(xq.split_cnt + pj, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   if (qq >= win_nrows[pj / H]) return;  // only the window's rows were recorded
-  float mv[XS_NSP], lv[XS_NSP];
-  float4_t ov[XS_NSP];
-#pragma unroll
-  for (int k = 0; k < XS_NSP; ++k) {  // every record load issued first (clamped index)
-    const int rb = (pj * nsp + min(k, nsp - 1)) * XREC * 4;
-    ov[k] = __builtin_bit_cast(float4_t, __builtin_amdgcn_raw_buffer_load_b128(rs, rb + (qq * 64 + dc) * 4, 0, 16));
-    mv[k] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, rb + (1024 + qq) * 4, 0, 16));
-    lv[k] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, rb + (1040 + qq) * 4, 0, 16));
-  }
-  emit(pj, xs_merge(nsp, mv, lv, ov));
+  emit(pj, xs_merge(nsp, [&](int k, float& m, float& l, float4_t& o) {
+         const int rb = (pj * nsp + k) * XREC * 4;
+         m = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, rb + (1024 + qq) * 4, 0, 16));
+         l = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, rb + (1040 + qq) * 4, 0, 16));
+         o = __builtin_bit_cast(float4_t, __builtin_amdgcn_raw_buffer_load_b128(rs, rb + (qq * 64 + dc) * 4, 0, 16));
+       }));
 }
 
-// Workgroups for nseg segments.  A CU streams its range with 8 waves that each take whole
-// segments, so the slowest wave sets the CU's time: the grid gives every wave the same
-// number of segments k = ceil(nseg / (256 x 8)) (the last workgroup excepted) rather than
-// filling all 256 CUs with uneven waves (20 windows: 200 workgroups of 24 segments, 3 per
-// wave, instead of 256 of 18-19 with 2 or 3 per wave).  k = 1 spreads the segments over
-// up to 256 workgroups (few windows: latency, not bandwidth).  Tuning builds:
-// WHISPER_HIP_XS_K forces k (read per launch).
-int xattn_seg_grid(int npair, int nsp) {
+// Workgroups for nseg = npair x nsp tiles (speed only; the numerics do not depend on it).
+//  * whole pairs per workgroup when that still fills >= 3/4 of the 256 CUs (20 windows:
+//    200 workgroups of 2 pairs): no pair is cut, so no records, counters or second merge;
+//  * else every wave gets the same number of tiles k = ceil(nseg / (256 x 8)) (the last
+//    workgroup excepted), cut pairs merged by the last arriver (15 windows: 225
+//    workgroups of 32 tiles rather than 150 of 2 pairs);
+//  * k = 1 spreads the tiles over up to 256 workgroups (few windows: latency).
+// Tuning builds: WHISPER_HIP_XS_K forces k (read per launch; disables the whole-pair rule).
+int xattn_seg_grid(int npair, int nsp, int smax) {
   const int nseg = npair * nsp;
-  int k = (nseg + 256 * 8 - 1) / (256 * 8);
+  int k = (nseg + 256 * 8 - 1) / (256 * 8), forced = 0;
   if (const char* e = tune_env("WHISPER_HIP_XS_K")) {
     const int v = atoi(e);
-    if (v >= 1) k = v;
+    if (v >= 1) k = v, forced = 1;
   }
-  if (k > XS_SMAX / 8) k = XS_SMAX / 8;
+  if (!forced && npair >= 192) {
+    const int ppw = (npair + 255) / 256, nwg = (npair + ppw - 1) / ppw;
+    if (nwg >= 192 && ppw * nsp <= smax) return nwg;
+  }
+  if (k > smax / 8) k = smax / 8;
   int nwg = k == 1 ? (nseg < 256 ? nseg : 256) : (nseg + 8 * k - 1) / (8 * k);
-  if ((nseg + nwg - 1) / nwg > XS_SMAX) nwg = (nseg + XS_SMAX - 1) / XS_SMAX;
+  if ((nseg + nwg - 1) / nwg > smax) nwg = (nseg + smax - 1) / smax;
   return nwg;
 }
 
@@ -1132,27 +1139,31 @@ void launch_cross_attn(const T* q, int ldq, const T* ck, const T* cv, int Tk, in
                        float* pm, float* pl, T* out, int ldo, int rows, float* qk_out, const int* qk_map, int qk_rows,
                        hipStream_t st, XQPart xq) {
   if (rows <= 0) return;
-  const int ntiles = (Tk + 63) / 64, nsp = ntiles / XS_T;
-  // the decoder step (<= 16 query rows per window, no alignment capture): segments
-  if (xq.max_rows >= 1 && xq.max_rows <= 16 && !qk_map && xq.split_rec && xq.split_cnt && ntiles % XS_T == 0 &&
-      nsp <= XS_NSP && nwin * H <= xq.max_pairs) {
-    const int npair = nwin * H, nwg = xattn_seg_grid(npair, nsp);
-#define XS(QZ_)                                                                                                  \
-  k_xattn_seg<T, QZ_><<<nwg, 512, 0, st>>>(q, ldq, ck, cv, Tk, H, npair, nsp, win_row0, win_nrows, win_slot, \
-                                           win_stride, xq, out, ldo)
+  const int nsp = (Tk + 63) / 64;
+  // the decoder step (<= 16 query rows per window, no alignment capture): tile partials
+  if (xq.max_rows >= 1 && xq.max_rows <= 16 && !qk_map && xq.split_rec && xq.split_cnt && nsp <= XS_NSP &&
+      nwin * H <= xq.max_pairs) {
+    const int npair = nwin * H;
+#define XS(QZ_, RR_)                                                                                              \
+  k_xattn_seg<T, QZ_, RR_><<<xattn_seg_grid(npair, nsp, XsShape<RR_>::SMAX), 512, 0, st>>>(                  \
+      q, ldq, ck, cv, Tk, H, npair, nsp, win_row0, win_nrows, win_slot, win_stride, xq, out, ldo)
+#define XSR(QZ_)                        \
+  if (xq.max_rows <= 8) XS(QZ_, 8);     \
+  else XS(QZ_, 16);
     switch (xq.part ? xq.z : 0) {
-      case 4: XS(4); break;
-      case 8: XS(8); break;
-      case 10: XS(10); break;
-      default: XS(0); break;
+      case 4: XSR(4) break;
+      case 8: XSR(8) break;
+      case 10: XSR(10) break;
+      default: XSR(0) break;
     }
+#undef XSR
 #undef XS
     return;
   }
   // first passes (prefill, alignment capture): one 64-key tile per wave, 8 waves per
   // split, partials combined by k_cross_combine
   constexpr int NW = 8;
-  nsplit = (ntiles + NW - 1) / NW;
+  nsplit = (nsp + NW - 1) / NW;
   const dim3 grid(nwin, H, nsplit);
 #define XA(QZ_)                                                                                          \
   k_cross_attn<T, NW, QZ_><<<grid, 64 * NW, 0, st>>>(q, ldq, ck, cv, Tk, H, nsplit, win_row0, win_nrows, win_slot, \

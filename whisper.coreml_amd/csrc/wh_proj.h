@@ -183,10 +183,17 @@ struct Proj1Shape {
   static constexpr int LDS = (XBYTES > RBYTES ? XBYTES : RBYTES) > 16 ? (XBYTES > RBYTES ? XBYTES : RBYTES) : 16;
 };
 
-template <typename T, int NSUB, int KW, int NSTEP, int ZS, int CPL, int EPI>
+// MODE bit 0 (P1_PEND, LayerNorm prologues): a deferred residual is pending on the input
+// rows (GemmArgs::res_slab); bit 1 (P1_DEFER, residual projections, ZS == 2): store the
+// two K-half slabs and stop — the next LayerNorm prologue adds them (no in-launch
+// reduction: no drain, counter or second slab read on this launch's critical path).
+constexpr int P1_PEND = 1, P1_DEFER = 2;
+
+template <typename T, int NSUB, int KW, int NSTEP, int ZS, int CPL, int EPI, int MODE>
 __global__ __launch_bounds__(64 * NSUB * KW) void k_proj1(GemmArgs a) {
   using P = Proj1Shape<T, NSUB, KW, NSTEP, CPL>;
   constexpr bool LN = CPL > 0;
+  constexpr bool PEND = LN && (MODE & P1_PEND), DEFER = (MODE & P1_DEFER) && ZS == 2 && EPI == EPI_RESID;
   constexpr int NWV = NSUB * KW;
   constexpr int RPW = (P1_RMAX + NWV - 1) / NWV;  // LayerNorm rows per wave
   extern __shared__ __attribute__((aligned(16))) char xs[];
@@ -202,6 +209,7 @@ __global__ __launch_bounds__(64 * NSUB * KW) void k_proj1(GemmArgs a) {
   // 1. activations (clamped addresses, no branch around a load)
   const int CH = K / 4;  // LN: float4 chunks per residual row
   float4_t xv[LN ? RPW : 1][LN ? CPL : 1], gv[LN ? CPL : 1], bv[LN ? CPL : 1];
+  float4_t s0v[PEND ? RPW : 1][PEND ? CPL : 1], s1v[PEND ? RPW : 1][PEND ? CPL : 1], rbv[PEND ? CPL : 1];
   Frag<T> xf[LN ? 1 : NSTEP];
   if constexpr (LN) {
 #pragma unroll
@@ -209,6 +217,21 @@ __global__ __launch_bounds__(64 * NSUB * KW) void k_proj1(GemmArgs a) {
       const float* xr = a.xf32 + (int64_t)min(wave + NWV * j, R - 1) * K;
 #pragma unroll
       for (int i = 0; i < CPL; ++i) xv[j][i] = load4f(xr + 4 * min(lane + 64 * i, CH - 1));
+    }
+    if constexpr (PEND) {
+      // the pending residual's two K-half slabs, row-major [2][R][K] like the rows
+#pragma unroll
+      for (int j = 0; j < RPW; ++j) {
+        const int row = min(wave + NWV * j, R - 1);
+#pragma unroll
+        for (int i = 0; i < CPL; ++i) {
+          const int off = row * K + 4 * min(lane + 64 * i, CH - 1);
+          s0v[j][i] = load4f(a.res_slab + off);
+          s1v[j][i] = load4f(a.res_slab + R * K + off);
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < CPL; ++i) rbv[i] = load4f(a.res_bias + 4 * min(lane + 64 * i, CH - 1));
     }
 #pragma unroll
     for (int i = 0; i < CPL; ++i) {
@@ -229,9 +252,9 @@ __global__ __launch_bounds__(64 * NSUB * KW) void k_proj1(GemmArgs a) {
   // the epilogue's operands ride in the same round trip: bias (every k_proj1 call has
   // one) and, for the residual add, this lane's x (only this tile's reducer writes it)
   const int n = n0 + 4 * g, re = min(r, R - 1);
-  const float4_t pre_b = load4f(a.bias + n);
-  float4_t pre_x = (float4_t){0.f, 0.f, 0.f, 0.f};
-  if constexpr (EPI == EPI_RESID) pre_x = load4f(a.out_f32 + (int64_t)re * a.ldo + n);
+  float4_t pre_b = (float4_t){0.f, 0.f, 0.f, 0.f}, pre_x = (float4_t){0.f, 0.f, 0.f, 0.f};
+  if constexpr (!DEFER) pre_b = load4f(a.bias + n);
+  if constexpr (EPI == EPI_RESID && !DEFER) pre_x = load4f(a.out_f32 + (int64_t)re * a.ldo + n);
   // every load above is issued before any wait (else hipcc streams them through a
   // sliding window of ~9, several round trips per wave)
   __builtin_amdgcn_sched_barrier(0);
@@ -239,6 +262,31 @@ __global__ __launch_bounds__(64 * NSUB * KW) void k_proj1(GemmArgs a) {
   // 3. LayerNorm of the full rows (biased variance, two passes in registers: the
   // arithmetic of k_layernorm); this workgroup's K range of it -> LDS
   if constexpr (LN) {
+    if constexpr (PEND) {
+      // x_new = x + ((slab0 + slab1) + bias): the order of the in-launch reduction
+#pragma unroll
+      for (int j = 0; j < RPW; ++j)
+#pragma unroll
+        for (int i = 0; i < CPL; ++i) {
+          float4_t t = s0v[j][i] + s1v[j][i];
+          t += rbv[i];
+          xv[j][i] += t;
+        }
+      if (blockIdx.x == 0 && blockIdx.y == 0) {  // one workgroup publishes x_new
+#pragma unroll
+        for (int j = 0; j < RPW; ++j) {
+          const int row = wave + NWV * j;
+          if (row < R) {
+#pragma unroll
+            for (int i = 0; i < CPL; ++i)
+              if (lane + 64 * i < CH) {
+                const float4_t v = xv[j][i];
+                store4(a.x_out + (int64_t)row * K + 4 * (lane + 64 * i), v[0], v[1], v[2], v[3]);
+              }
+          }
+        }
+      }
+    }
 #pragma unroll
     for (int j = 0; j < RPW; ++j) {
       const int row = wave + NWV * j;
@@ -309,6 +357,10 @@ __global__ __launch_bounds__(64 * NSUB * KW) void k_proj1(GemmArgs a) {
     typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
     const int ntile = gridDim.x * NSUB;
     const auto rs = __builtin_amdgcn_make_buffer_rsrc(a.p1_slab, 0, 0x7fffffff, 0x00020000);
+    if constexpr (DEFER) {  // row-major [2][R][N] for the next LayerNorm prologue, which sums them
+      if (r < R) store4(a.p1_slab + ((int64_t)kz * R + r) * a.N + n, acc[0], acc[1], acc[2], acc[3]);
+      return;
+    }
     __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc), rs, ((kz * ntile + tile) * 256 + lane * 4) * 4,
                                            0, 16);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");

@@ -131,15 +131,16 @@ int launch_proj_partial(const GemmArgs& a, int max_z, hipStream_t st, int* z_out
 // against 5.5 / 8.0 / 8.3 / 5.4 / 5.7 us for the tilings here, which split only the
 // residual projections, in two.
 namespace {
-template <typename T, int NSUB, int KW, int NS, int ZS, int CPL, int EPI>
+template <typename T, int NSUB, int KW, int NS, int ZS, int CPL, int EPI, int MODE = 0>
 int p1_go(const GemmArgs& a, hipStream_t st, hipEvent_t ev0, hipEvent_t ev1) {
   using P = Proj1Shape<T, NSUB, KW, NS, CPL>;
   static_assert(P::LDS <= 64 * 1024, "k_proj1 LDS");
   static_assert(NSUB * KW <= 16, "k_proj1 waves");
   if (a.K != ZS * P::KC || a.N % (16 * NSUB)) return -1;
   if (ZS > 1 && (!a.p1_slab || !a.p1_cnt || (int64_t)ZS * (a.N / 16) > a.p1_slabs)) return -1;
+  if ((MODE & P1_PEND) && (!a.res_slab || !a.res_bias || !a.x_out || a.x_out == a.xf32)) return -1;
   const dim3 grid(a.N / (16 * NSUB), ZS), block(64 * NSUB * KW);
-  void (*f)(GemmArgs) = &k_proj1<T, NSUB, KW, NS, ZS, CPL, EPI>;
+  void (*f)(GemmArgs) = &k_proj1<T, NSUB, KW, NS, ZS, CPL, EPI, MODE>;
   if (ev0)
     hipExtLaunchKernelGGL(f, grid, block, P::LDS, st, ev0, ev1, 0, a);
   else
@@ -152,12 +153,24 @@ template <typename T, int CPL, int BKW, int NS, int F1SUB>
 int p1_width_launch(const GemmArgs& a, int epi, bool ln, int n, hipStream_t st, hipEvent_t e0, hipEvent_t e1) {
   if (ln) {
     if (a.K != n) return -1;
+    if (a.res_slab) {  // a deferred residual is pending on the input rows
+      if (epi == EPI_QKV_DEC && a.N == 3 * n) return p1_go<T, 1, BKW, NS, 1, CPL, EPI_QKV_DEC, P1_PEND>(a, st, e0, e1);
+      if (epi == EPI_STORE_GELU && a.N == 4 * n)
+        return p1_go<T, F1SUB, BKW, NS, 1, CPL, EPI_STORE_GELU, P1_PEND>(a, st, e0, e1);
+      if (epi == EPI_STORE && a.N == n) return p1_go<T, 1, BKW, NS, 1, CPL, EPI_STORE, P1_PEND>(a, st, e0, e1);
+      return -1;
+    }
     if (epi == EPI_QKV_DEC && a.N == 3 * n) return p1_go<T, 1, BKW, NS, 1, CPL, EPI_QKV_DEC>(a, st, e0, e1);
     if (epi == EPI_STORE_GELU && a.N == 4 * n) return p1_go<T, F1SUB, BKW, NS, 1, CPL, EPI_STORE_GELU>(a, st, e0, e1);
     if (epi == EPI_STORE && a.N == n) return p1_go<T, 1, BKW, NS, 1, CPL, EPI_STORE>(a, st, e0, e1);
     return -1;
   }
   if (epi != EPI_RESID || a.N != n) return -1;
+  if (a.p1_defer) {
+    if (a.K == n) return p1_go<T, 1, BKW / 2, NS, 2, 0, EPI_RESID, P1_DEFER>(a, st, e0, e1);
+    if (a.K == 4 * n) return p1_go<T, 1, 2 * BKW, NS, 2, 0, EPI_RESID, P1_DEFER>(a, st, e0, e1);
+    return -1;
+  }
   if (a.K == n) return p1_go<T, 1, BKW / 2, NS, 2, 0, EPI_RESID>(a, st, e0, e1);
   if (a.K == 4 * n) return p1_go<T, 1, 2 * BKW, NS, 2, 0, EPI_RESID>(a, st, e0, e1);
   return -1;

@@ -188,6 +188,7 @@ struct Ctx : public wh_ctx {
   float* p1_slab = nullptr;  // k_proj1 in-launch split-K slabs [zs][N/16][256]
   int* p1_cnt = nullptr;     // and arrival counters [4n/16] (zero between launches)
   float* xs_rec = nullptr;   // step cross-attention segment records [pair][XS_NSP][XREC]
+  float* x2_d = nullptr;     // k_proj1 path: second residual buffer (deferred residual ping-pong)
   int* xs_cnt = nullptr;     // and (window, head) arrival counters
 
   // the step cross-attention's query / split arguments
@@ -332,6 +333,7 @@ struct Ctx : public wh_ctx {
     addA(64);
     addA((size_t)P1_SLABS * 256 * 4); addA((size_t)(4 * n / 16) * 4);  // k_proj1 split-K slabs + counters
     addA((size_t)Wcap * nh * XS_NSP * XREC * 4); addA((size_t)Wcap * nh * 4);  // cross-attention segment records
+    addA((size_t)8 * n * 4);  // k_proj1 path (<= 8 rows, wh_proj.h P1_RMAX): the second residual buffer
     HIPCHK(hipMalloc(&abase, ab));
     HIPCHK(hipMemset(abase, 0, ab));
     aa.base = (char*)abase;
@@ -366,7 +368,8 @@ struct Ctx : public wh_ctx {
     S.seed = (unsigned long long*)aa.take(64);
     p1_slab = fa((size_t)P1_SLABS * 256); p1_cnt = ia(4 * n / 16);  // zeroed with the arena
     xs_rec = fa((size_t)Wcap * nh * XS_NSP * XREC); xs_cnt = ia((size_t)Wcap * nh);
-    if (!S.seed || !S.cand_idx || !p1_cnt || !xs_cnt) return fail(-3, "activation arena overflow");
+    x2_d = fa((size_t)8 * n);
+    if (!S.seed || !S.cand_idx || !p1_cnt || !xs_cnt || !x2_d) return fail(-3, "activation arena overflow");
     S.nw = Wcap; S.G = 1; S.ctx = CTX; S.hctx = HCTX; S.maxc = 16;
     HIPCHK(hipMalloc(&d_gmax, 64));
     d_gmax_f = (float*)(d_gmax + 4);
@@ -893,42 +896,64 @@ struct Ctx : public wh_ctx {
   int dec_layers_p1(int R, const int* rw, const int* rs, const int* rp, int ancG, int nwin, const int* wr0,
                     const int* wnr, const int* wsl) {
     const int n = ns;
+    // deferred residual: fc2 stores its two K-half slabs only; the next layer's QKV
+    // LayerNorm prologue adds them (+ bias) to the current rows and one of its workgroups
+    // publishes the sum into the other buffer, which becomes current (fc2 7.9 -> 5.9 us,
+    // the QKV prologue +0.6; profiles/r03/step_w1_p1def_summary.txt)
+    float* xc = x_d;
+    float* xo = x2_d;
+    const float* pend = nullptr;  // bias of the residual pending in p1_slab
+    auto ln_in = [&](GemmArgs& g, const float* lg, const float* lb) {
+      g.xf32 = xc; g.ln_g = lg; g.ln_b = lb; g.ln_eps = 1e-5f;
+      if (pend) { g.res_slab = p1_slab; g.res_bias = pend; g.x_out = xo; }
+    };
+    auto ln_done = [&]() {
+      if (pend) { std::swap(xc, xo); pend = nullptr; }
+    };
+    auto resid = [&](const T* X, int K, const T* W, const float* b, bool defer) -> int {
+      GemmArgs g;
+      g.X = X; g.ldx = K; g.W = W; g.bias = b; g.M = R; g.N = n; g.K = K; g.out_f32 = xc; g.ldo = n;
+      g.p1_defer = defer;
+      TRY(p1(g, EPI_RESID, false));
+      if (defer) pend = b;
+      return 0;
+    };
     for (int l = 0; l < Ld; ++l) {
       auto& e = dec[l];
       // self-attention block: q, k, v of LN1(x) (k / v straight into the cache)
       GemmArgs g;
       g.W = e.wqkv; g.bias = e.bqkv; g.M = R; g.N = 3 * n; g.K = n;
-      g.xf32 = x_d; g.ln_g = e.ln1_g; g.ln_b = e.ln1_b; g.ln_eps = 1e-5f;
+      ln_in(g, e.ln1_g, e.ln1_b);
       g.out = q_d; g.ldo = n; g.hs_state = n; g.hs_heads = nh;
       g.row_win = rw; g.row_slot = rs; g.row_pos = rp; g.kc = kc[l]; g.vc = vc[l]; g.kv_beams = Gcap; g.kv_ctx = CTX;
       TRY(p1(g, EPI_QKV_DEC, true));
+      ln_done();
       launch_self_attn<T>(q_d, n, kc[l], vc[l], rw, rs, rp, S.anc, ancG, Gcap, nh, CTX, att_d, n, R, st);
-      g = GemmArgs();
-      g.X = att_d; g.ldx = n; g.W = e.wo; g.bias = e.bo; g.M = R; g.N = n; g.K = n; g.out_f32 = x_d; g.ldo = n;
-      TRY(p1(g, EPI_RESID, false));
+      TRY(resid(att_d, n, e.wo, e.bo, false));  // deferring it measured +1.0 us on cross-q, -0.2 here
       // cross-attention block
       g = GemmArgs();
       g.W = e.wqx; g.bias = e.bqx; g.M = R; g.N = n; g.K = n;
-      g.xf32 = x_d; g.ln_g = e.lnx_g; g.ln_b = e.lnx_b; g.ln_eps = 1e-5f; g.out = q_d; g.ldo = n;
+      ln_in(g, e.lnx_g, e.lnx_b);
+      g.out = q_d; g.ldo = n;
       TRY(p1(g, EPI_STORE, true));
+      ln_done();
       const XQPart xq = step_xq(ancG);
       const T* ck = ckv + (size_t)(2 * l) * Wcap * TKP * n;
       const T* cv = ckv + (size_t)(2 * l + 1) * Wcap * TKP * n;
       launch_cross_attn<T>(q_d, n, ck, cv, 1500, nh, NSPLIT, nwin, wr0, wnr, wsl, (int64_t)TKP * n, po, pm, pl, att_d,
                            n, R, nullptr, nullptr, 0, st, xq);
-      g = GemmArgs();
-      g.X = att_d; g.ldx = n; g.W = e.wox; g.bias = e.box; g.M = R; g.N = n; g.K = n; g.out_f32 = x_d; g.ldo = n;
-      TRY(p1(g, EPI_RESID, false));
-      // MLP
+      // (not deferred: fc1's 16-wave LayerNorm prologue has no registers for two more row copies)
+      TRY(resid(att_d, n, e.wox, e.box, false));
+      // MLP; the last layer's fc2 reduces in-launch (the final LayerNorm reads x)
       g = GemmArgs();
       g.W = e.w1; g.bias = e.b1; g.M = R; g.N = 4 * n; g.K = n;
-      g.xf32 = x_d; g.ln_g = e.ln2_g; g.ln_b = e.ln2_b; g.ln_eps = 1e-5f; g.out = hm_d; g.ldo = 4 * n;
+      ln_in(g, e.ln2_g, e.ln2_b);
+      g.out = hm_d; g.ldo = 4 * n;
       TRY(p1(g, EPI_STORE_GELU, true));
-      g = GemmArgs();
-      g.X = hm_d; g.ldx = 4 * n; g.W = e.w2; g.bias = e.b2; g.M = R; g.N = n; g.K = 4 * n; g.out_f32 = x_d; g.ldo = n;
-      TRY(p1(g, EPI_RESID, false));
+      ln_done();
+      TRY(resid(hm_d, 4 * n, e.w2, e.b2, l + 1 < Ld));
     }
-    launch_layernorm<T>(x_d, xn_d, ln_g, ln_b, R, n, 1e-5f, nullptr, st);
+    launch_layernorm<T>(xc, xn_d, ln_g, ln_b, R, n, 1e-5f, nullptr, st);
     return 0;
   }
 
