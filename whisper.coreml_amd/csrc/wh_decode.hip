@@ -6,7 +6,7 @@
 //   GreedyDecoder.update                                  (decoding.py:304-320)
 //   BeamSearchDecoder.update incl. finished bookkeeping   (decoding.py:350-409)
 //   PyTorchInference.rearrange_kv_cache                   (decoding.py:189-204) -> index indirection
-// k_logit_part + k_logit_combine (default): 8 vocabulary slices per row, one workgroup
+// k_logit_part + k_logit_combine (default): 8 or 32 vocabulary slices per row, one workgroup
 //               each, then one wave per row merging the kept slices.
 // k_logit_rows: the single-workgroup form (one 1024-thread workgroup per decoder row;
 //               WHISPER_HIP_LOGIT_SPLIT=0).
@@ -298,8 +298,8 @@ __global__ __launch_bounds__(LR_THREADS) void k_logit_rows(float* __restrict__ l
 }
 
 // ---------------------------------------------------------------- split selection
-// The same selection with each row's vocabulary in LP_SLICES slices, one 512-thread
-// workgroup per (row, slice): slices 0..LP_SLICES-2 split the text ids [0, ts_begin),
+// The same selection with each row's vocabulary in NS slices, one 512-thread
+// workgroup per (row, slice): slices 0..NS-2 split the text ids [0, ts_begin),
 // the last one is the timestamp range [ts_begin, V) on its own, so the
 // ApplyTimestampRules tail (decoding.py:522-531: logsumexp over timestamps vs the text
 // maximum) and the masking of text it may decide are both per-slice facts the combine
@@ -314,7 +314,10 @@ constexpr int LP_THREADS = 512;
 #else
 #define WH_LP_ATTR
 #endif
-constexpr int LP_EPT = 16;  // elements per lane: 512 x 16 >= every slice
+// NS slices per row (NS - 1 text slices + the timestamp range) with EPT elements per lane:
+// 32 slices (EPT 4: ceil(50365 / 31) = 1625 and 1501 <= 512 x 4) for few rows, where the
+// per-workgroup latency is the cost (1 window: 29.9 -> 14.4 us); 8 slices (EPT 16) for
+// many rows, where 32 x rows workgroups cost more than they hide (100 rows: 54 vs 62 us)
 
 struct LPRec {
   float mx, se, bv, gv, gx;
@@ -325,10 +328,10 @@ struct LPRec {
 };
 static_assert(sizeof(LPRec) == LP_REC * 4, "slice record stride");
 
-__device__ __forceinline__ void lp_slice(int j, int tb, int V, int& lo, int& hi) {
-  if (j == LP_SLICES - 1) { lo = tb; hi = V; return; }
-  lo = (int)((int64_t)tb * j / (LP_SLICES - 1));
-  hi = (int)((int64_t)tb * (j + 1) / (LP_SLICES - 1));
+__device__ __forceinline__ void lp_slice(int j, int ns, int tb, int V, int& lo, int& hi) {
+  if (j == ns - 1) { lo = tb; hi = V; return; }
+  lo = (int)((int64_t)tb * j / (ns - 1));
+  hi = (int)((int64_t)tb * (j + 1) / (ns - 1));
 }
 
 // wave-level (value desc, index asc) argbest; every lane ends with the winner
@@ -346,6 +349,7 @@ __device__ __forceinline__ void wave_argbest(float& v, int& idx) {
 // argbest / Gumbel best); wave 0 then merges the 8 wave results and writes the record.
 // The slice's logits and suppress words are loaded first, before the history, so their
 // round trip overlaps it.
+template <int NS, int LP_EPT>
 __global__ __launch_bounds__(LP_THREADS) WH_LP_ATTR void k_logit_part(float* __restrict__ logits, int ldl, DecState s,
                                                            DecOpts o) {
   constexpr int NWV = LP_THREADS / 64;
@@ -356,7 +360,7 @@ __global__ __launch_bounds__(LP_THREADS) WH_LP_ATTR void k_logit_part(float* __r
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int V = o.V, tb = o.ts_begin;
   int lo, hi;
-  lp_slice(j, tb, V, lo, hi);
+  lp_slice(j, NS, tb, V, lo, hi);
   float* row = logits + (int64_t)r * ldl;
   // 1. this slice's logits and suppress words (clamped addresses, masked below)
   float xv[LP_EPT];
@@ -434,7 +438,7 @@ __global__ __launch_bounds__(LP_THREADS) WH_LP_ATTR void k_logit_part(float* __r
   }
   se = wave_sum(se);
   if (lane == 0) { wmx[wv] = mx; wse[wv] = se; }
-  LPRec* rec = reinterpret_cast<LPRec*>(s.lpart + ((int64_t)r * LP_SLICES + j) * LP_REC);
+  LPRec* rec = reinterpret_cast<LPRec*>(s.lpart + ((int64_t)r * LP_SLICES + j) * LP_REC);  // NS <= LP_SLICES
   const int need = s.G + 1;
   if (!o.beam) {
     float bv = -INFINITY, gv = -INFINITY, gx = -INFINITY;
@@ -543,14 +547,15 @@ __global__ __launch_bounds__(LP_THREADS) WH_LP_ATTR void k_logit_part(float* __r
   if (lane == 0) { rec->mx = MX; rec->se = SE; }
 }
 
+template <int NS>
 __global__ __launch_bounds__(64) void k_logit_combine(DecState s, DecOpts o) {
   const int r = blockIdx.x, w = r / s.G, lane = threadIdx.x;
   // the row's slice records -> LDS in one round trip, issued with the done flag's load
   // (the merge below reads them serially; from global memory every read would be a
   // dependent load)
-  __shared__ __attribute__((aligned(16))) float recs[LP_SLICES * LP_REC];
+  __shared__ __attribute__((aligned(16))) float recs[NS * LP_REC];
   {
-    constexpr int N4 = LP_SLICES * LP_REC / 4, PER = (N4 + 63) / 64;
+    constexpr int N4 = NS * LP_REC / 4, PER = (N4 + 63) / 64;
     const float4_t* src = reinterpret_cast<const float4_t*>(s.lpart + (int64_t)r * LP_SLICES * LP_REC);
     float4_t* dst = reinterpret_cast<float4_t*>(recs);
     float4_t v[PER];
@@ -563,13 +568,13 @@ __global__ __launch_bounds__(64) void k_logit_combine(DecState s, DecOpts o) {
   }
   __syncthreads();
   const LPRec* rec = reinterpret_cast<const LPRec*>(recs);
-  constexpr int TS = LP_SLICES - 1;
+  constexpr int TS = NS - 1;
   float m = -INFINITY;
-  for (int j = 0; j < LP_SLICES; ++j) m = fmaxf(m, rec[j].mx);
+  for (int j = 0; j < NS; ++j) m = fmaxf(m, rec[j].mx);
   bool text_killed = false;
   if (o.timestamps) {
     float st0 = 0.f, mx_tx = -INFINITY;
-    for (int j = 0; j < LP_SLICES; ++j)
+    for (int j = 0; j < NS; ++j)
       if (rec[j].mx > -INFINITY) st0 += rec[j].se * __expf(rec[j].mx - m);
     for (int j = 0; j < TS; ++j) mx_tx = fmaxf(mx_tx, rec[j].mx);
     const float lS0 = logf(st0), mx_ts = rec[TS].mx;
@@ -582,43 +587,48 @@ __global__ __launch_bounds__(64) void k_logit_combine(DecState s, DecOpts o) {
   }
   const int j0 = text_killed ? TS : 0;
   float se = 0.f;
-  for (int j = j0; j < LP_SLICES; ++j)
+  for (int j = j0; j < NS; ++j)
     if (rec[j].mx > -INFINITY) se += rec[j].se * __expf(rec[j].mx - m);
   const float logS = logf(se);
   float* cv = s.cand_val + (int64_t)r * KC;
   int* ci = s.cand_idx + (int64_t)r * KC;
+  // lane j holds slice j (NS <= 64): wave-level argbest rounds, the order of better()
+  // (value desc, index asc) as in the slices themselves
+  static_assert(NS <= 64 && NS <= LP_SLICES, "one lane per slice");
+  const bool act = lane < NS && lane >= j0;
   if (!o.beam) {
-    if (lane != 0) return;
     float bv = -INFINITY, bx = -INFINITY;
     int bi = 0x7fffffff;
-    for (int j = j0; j < LP_SLICES; ++j) {
-      if (o.temperature > 0.f) {
-        if (better(rec[j].gv, rec[j].gi, bv, bi)) { bv = rec[j].gv; bi = rec[j].gi; bx = rec[j].gx; }
-      } else if (better(rec[j].bv, rec[j].bi, bv, bi)) {
-        bv = rec[j].bv; bi = rec[j].bi; bx = rec[j].bv;
-      }
+    if (act) {
+      if (o.temperature > 0.f) { bv = rec[lane].gv; bi = rec[lane].gi; bx = rec[lane].gx; }
+      else { bv = rec[lane].bv; bi = rec[lane].bi; bx = bv; }
     }
-    if (bi != 0x7fffffff) {
+    const int mine = bi;
+    const float myx = bx;
+    wave_argbest(bv, bi);
+    const unsigned long long own = __ballot(mine == bi && bi != 0x7fffffff);
+    const float wx = own ? __shfl(myx, __ffsll((long long)own) - 1, 64) : -INFINITY;
+    if (lane == 0 && bi != 0x7fffffff) {
       ci[0] = bi;
-      cv[0] = (bx - m) - logS;
+      cv[0] = (wx - m) - logS;
     }
     return;
   }
-  // merge the kept slices' sorted top lists (lane 0; at most 8 x 9 candidates)
-  if (lane != 0) return;
+  // beam: merge the kept slices' sorted top lists, one head per lane
   const int need = s.G + 1;
-  int hd[LP_SLICES];
-  for (int j = 0; j < LP_SLICES; ++j) hd[j] = 0;
+  int hd = 0;
   for (int q = 0; q < need; ++q) {
-    float bv = -INFINITY;
-    int bi = 0x7fffffff, bj = -1;
-    for (int j = j0; j < LP_SLICES; ++j)
-      if (hd[j] < need && better(rec[j].tv[hd[j]], rec[j].ti[hd[j]], bv, bi)) {
-        bv = rec[j].tv[hd[j]]; bi = rec[j].ti[hd[j]]; bj = j;
-      }
-    if (bj >= 0 && bi != 0x7fffffff) ++hd[bj];
-    cv[q] = (bv - m) - logS;
-    ci[q] = bi;
+    float hv = -INFINITY;
+    int hi = 0x7fffffff;
+    if (act && hd < need) { hv = rec[lane].tv[hd]; hi = rec[lane].ti[hd]; }
+    float bv = hv;
+    int bi = hi;
+    wave_argbest(bv, bi);
+    if (bi == hi && bi != 0x7fffffff) ++hd;
+    if (lane == 0) {
+      cv[q] = (bv - m) - logS;
+      ci[q] = bi;
+    }
   }
 }
 
@@ -629,10 +639,15 @@ void launch_logit_rows(float* logits, int ldl, const DecState& s, const DecOpts&
     const char* e = tune_env("WHISPER_HIP_LOGIT_SPLIT");
     return !(e && e[0] == '0');
   }();
-  const int slice_max = (o.ts_begin + LP_SLICES - 2) / (LP_SLICES - 1);
-  if (split && slice_max <= LP_THREADS * LP_EPT && o.V - o.ts_begin <= LP_THREADS * LP_EPT && o.ts_begin > 0) {
-    k_logit_part<<<dim3(nwin * s.G, LP_SLICES), LP_THREADS, 0, st>>>(logits, ldl, s, o);
-    k_logit_combine<<<nwin * s.G, 64, 0, st>>>(s, o);
+  const int rows = nwin * s.G;
+  if (split && o.ts_begin > 0 && rows <= 32 && (o.ts_begin + 30) / 31 <= LP_THREADS * 4 && o.V - o.ts_begin <= LP_THREADS * 4) {
+    k_logit_part<32, 4><<<dim3(rows, 32), LP_THREADS, 0, st>>>(logits, ldl, s, o);
+    k_logit_combine<32><<<rows, 64, 0, st>>>(s, o);
+    return;
+  }
+  if (split && o.ts_begin > 0 && (o.ts_begin + 6) / 7 <= LP_THREADS * 16 && o.V - o.ts_begin <= LP_THREADS * 16) {
+    k_logit_part<8, 16><<<dim3(rows, 8), LP_THREADS, 0, st>>>(logits, ldl, s, o);
+    k_logit_combine<8><<<rows, 64, 0, st>>>(s, o);
     return;
   }
   k_logit_rows<<<nwin * s.G, LR_THREADS, 0, st>>>(logits, ldl, s, o);

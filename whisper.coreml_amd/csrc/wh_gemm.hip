@@ -440,7 +440,53 @@ __global__ __launch_bounds__(512) void k_vocab_small(GemmArgs a) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = lane & 15, g = lane >> 4;
   const T* X = reinterpret_cast<const T*>(a.X);
   const T* W = reinterpret_cast<const T*>(a.W);
-  {  // stage X rows (rows >= M: zeros)
+  if (a.xf32) {
+    // the decoder's final LayerNorm (decoder.py:316) of the fp32 residual rows, recomputed
+    // by every workgroup (<= 8 rows x K x 4 B from L2) instead of its own launch: one wave
+    // per row, two passes in registers (the arithmetic of k_layernorm / k_proj1)
+    constexpr int CPLM = 5;  // float4 chunks per lane: K <= 1280
+    const int CH = K / 4;
+    for (int row = wave; row < MT * 16; row += 8) {
+      T* dst = reinterpret_cast<T*>(xsv + row * xrow);
+      if (row >= a.M) {
+        for (int c = lane; c < CH; c += 64) store4(dst + 4 * c, 0.f, 0.f, 0.f, 0.f);
+        continue;
+      }
+      const float* xr = a.xf32 + (int64_t)row * K;
+      float4_t xv[CPLM], gv[CPLM], bv[CPLM];
+#pragma unroll
+      for (int i = 0; i < CPLM; ++i) {
+        const int c = min(lane + 64 * i, CH - 1);
+        xv[i] = load4f(xr + 4 * c);
+        gv[i] = load4f(a.ln_g + 4 * c);
+        bv[i] = load4f(a.ln_b + 4 * c);
+      }
+      float sm = 0.f;
+#pragma unroll
+      for (int i = 0; i < CPLM; ++i)
+        if (lane + 64 * i < CH) sm += xv[i][0] + xv[i][1] + xv[i][2] + xv[i][3];
+      const float mean = wave_sum(sm) / (float)K;
+      float q = 0.f;
+#pragma unroll
+      for (int i = 0; i < CPLM; ++i)
+        if (lane + 64 * i < CH) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float d = xv[i][e] - mean;
+            q += d * d;
+          }
+        }
+      const float rstd = rsqrtf(wave_sum(q) / (float)K + a.ln_eps);
+#pragma unroll
+      for (int i = 0; i < CPLM; ++i)
+        if (lane + 64 * i < CH) {
+          const float4_t v = xv[i];
+          store4(dst + 4 * (lane + 64 * i), (v[0] - mean) * rstd * gv[i][0] + bv[i][0],
+                 (v[1] - mean) * rstd * gv[i][1] + bv[i][1], (v[2] - mean) * rstd * gv[i][2] + bv[i][2],
+                 (v[3] - mean) * rstd * gv[i][3] + bv[i][3]);
+        }
+    }
+  } else {  // stage X rows (rows >= M: zeros)
     const int cpr = K * (int)sizeof(T) / 16, total = MT * 16 * cpr;
     for (int c = tid; c < total; c += 512) {
       const int row = c / cpr, col = c - row * cpr;
@@ -720,6 +766,9 @@ int launch_gemm_tiles(const GemmArgs& a, int epi, int tile_sel, hipStream_t st) 
       const char* e = tune_env("WHISPER_HIP_VOCAB_SMALL");
       return !(e && e[0] == '0');
     }();
+    if (a.xf32 && !(vocab_small && epi == EPI_F32_COLS && a.N >= 16384 && a.M <= 8 && a.K <= 1280 && a.K % 32 == 0 &&
+                    !a.x_rows))
+      return -6;  // the LayerNorm prologue exists only in k_vocab_small
     if (vocab_small && epi == EPI_F32_COLS && a.N >= 16384 && a.M <= (sizeof(T) == 2 ? 32 : 16) && a.K <= 1280 &&
         a.K % 32 == 0) {
       const int mtv = (a.M + 15) / 16;

@@ -101,7 +101,7 @@ struct DecOpts {
   float temperature;                 // > 0: Gumbel-max sampling (greedy decoder)
 };
 
-constexpr int LP_SLICES = 8;  // vocabulary slices per row: 7 text slices + [timestamp_begin, V)
+constexpr int LP_SLICES = 32;  // vocabulary slices per row: 31 text slices + [timestamp_begin, V)
 constexpr int LP_REC = 32;    // words per slice record
 void launch_logit_rows(float* logits, int ldl, const DecState& s, const DecOpts& o, int nwin, hipStream_t st);
 void launch_merge(const DecState& s, const DecOpts& o, int nwin, hipStream_t st);

@@ -85,7 +85,7 @@ int launch_proj_partial(const GemmArgs& a, int max_z, hipStream_t st, int* z_out
     const Cfg& k = CFGS[c];
     if (S % (k.kw * k.nstep)) continue;
     const int z = S / (k.kw * k.nstep);
-    if (z > max_z || z > 16 || tab.e[mt - 1][c].lds > LDS_MAX) continue;
+    if (z > 16 || tab.e[mt - 1][c].lds > LDS_MAX) continue;
     const int wgs = (a.N + 16 * k.nsub - 1) / (16 * k.nsub) * z;
     if (forced >= 0) {
       if (c == forced) best = c, best_wgs = wgs, best_z = z;
@@ -101,7 +101,10 @@ int launch_proj_partial(const GemmArgs& a, int max_z, hipStream_t st, int* z_out
         (deep == bdeep && (wgs > best_wgs || (wgs == best_wgs && k.nstep > CFGS[best].nstep))))
       best = c, best_wgs = wgs, best_z = z;
   }
-  if (best < 0) return -1;
+  // the tiling (and so every row's summation order) is chosen from the weight shape
+  // alone, never from the row count: a window's step is batch-invariant.
+  // max_z is only the slab capacity the caller has for this row count
+  if (best < 0 || best_z > max_z) return -1;
   const Ent& e = tab.e[mt - 1][best];
   if (!tab.attr[mt - 1][best]) {
     if (hipFuncSetAttribute(reinterpret_cast<const void*>(e.f), hipFuncAttributeMaxDynamicSharedMemorySize, e.lds) !=

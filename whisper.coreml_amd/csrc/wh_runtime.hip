@@ -775,6 +775,7 @@ struct Ctx : public wh_ctx {
     // split-K into fp32 partial slabs; QKV's reduction is fused into self-attention
     const bool skinny = step && R <= 128;
     GemmArgs g;
+    final_x = nullptr;
     if (step && !qkmap && p1_active(R))
       return dec_layers_p1(R, rw, rs, rp, ancG, nwin, wr0, wnr, wsl);
     launch_layernorm<T>(x_d, xn_d, dec[0].ln1_g, dec[0].ln1_b, R, n, 1e-5f, nullptr, st);
@@ -953,15 +954,22 @@ struct Ctx : public wh_ctx {
       ln_done();
       TRY(resid(hm_d, 4 * n, e.w2, e.b2, l + 1 < Ld));
     }
-    launch_layernorm<T>(xc, xn_d, ln_g, ln_b, R, n, 1e-5f, nullptr, st);
+    // the final LayerNorm runs in the vocabulary kernel's prologue (vocab(), final_x)
+    final_x = xc;
     return 0;
   }
 
   // logits = LN(x) E^T for R rows of xn_d (optionally gathered by rows_sel)
   // (decoder.py:238-240, 316-320)
+  // (after dec_layers_p1, final_x names the fp32 residual rows whose final LayerNorm
+  // k_vocab_small computes itself: no separate LayerNorm launch per token)
+  const float* final_x = nullptr;
   int vocab(const int* rows_sel, int R, float* out) {
     GemmArgs g;
     g.out_f32 = out; g.ldo = V; g.x_rows = rows_sel;
+    if (final_x && !rows_sel) {
+      g.xf32 = final_x; g.ln_g = ln_g; g.ln_b = ln_b; g.ln_eps = 1e-5f;
+    }
     return gemm(xn_d, ns, E, nullptr, R, V, ns, EPI_F32_COLS, g);
   }
 
