@@ -33,8 +33,8 @@ KERNELS = {
     # short name -> regex on the mangled kernel name
     "k_proj": r"k_projIDF16_",                # fp16 split-K projections (all tile variants), 100 rows
     "k_proj1": r"k_proj1IDF16_",              # single-window projections (5 rows, all six shapes)
-    "k_cross_attn1": r"k_cross_attn1IDF16_",  # the step's cross-attention, <= 12 windows
-    "k_cross_attn_bal": r"k_cross_attn_balIDF16_",  # the step's cross-attention, 13+ windows (20: bench)
+    "k_xattn_seg": r"k_xattn_segIDF16_",      # the step's cross-attention (round 3), 20 windows
+    "k_resid_ln": r"k_resid_lnIDF16_",        # split-K reduction + residual + LayerNorm, 100 rows
     "k_gemm_256": r"k_gemm_256",              # encoder GEMMs of the 20-window encode (all epilogues)
 }
 
@@ -55,6 +55,7 @@ def run():
     model.ctx.decode_begin(task.wh_opts(), [task.initial_tokens] * 20, [task.sot_index] * 20)
     print("gemv ms/launch", model.ctx.time_stage(2, 1))
     print("cross-attn ms/launch", model.ctx.time_stage(3, 1))
+    print("step ms", model.ctx.time_stage(0, 2))  # k_resid_ln (and every step kernel) in the graph
     # one window (5 rows): the six projections of every layer as k_proj1 launches
     model.ctx.decode_begin(task.wh_opts(), [task.initial_tokens], [task.sot_index])
     print("k_proj1 ms/launch", model.ctx.time_stage(2, 1))

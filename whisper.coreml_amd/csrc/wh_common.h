@@ -26,6 +26,7 @@ typedef float float4_t __attribute__((ext_vector_type(4)));
 typedef float float8_t __attribute__((ext_vector_type(8)));
 
 #define WH_DEV __device__ __forceinline__
+#define WH_DEV_HOST __host__ __device__ __forceinline__
 
 // Tuning switches (WHISPER_HIP_* environment variables that select measured-but-not-
 // adopted kernel variants for A/B runs) are read only by the tuning build
@@ -43,6 +44,15 @@ static inline const char* tune_env(const char* name) {
   return nullptr;
 #endif
 }
+
+// cross-V (V^T) of a (window, head) is TILE-MAJOR: [TKP / 64 tiles][64 d][64 keys, 32-key permutation],
+// so one 64-key tile's V^T is 8 KB contiguous (one stream, like K's [TKP][64] rows); element (d, t)
+// sits at xv_index(d, t).
+WH_DEV_HOST int xv_perm(int t) {
+  const int q = t & 31;
+  return (t & ~31) + 8 * ((q & 15) >> 2) + 4 * (q >> 4) + (q & 3);
+}
+WH_DEV_HOST int64_t xv_index(int d, int t) { return ((int64_t)(t >> 6) * 64 + d) * 64 + xv_perm(t & 63); }
 
 // ---------------------------------------------------------------- fragments
 template <typename T> struct Frag;

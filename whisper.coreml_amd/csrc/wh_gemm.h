@@ -83,19 +83,18 @@ WH_DEV void epilogue_store(const GemmArgs& a, int m, int gi, int ri, int n, floa
     float* o = a.out_f32 + (int64_t)m * a.ldo + n;
     store4(o, gelu_f(v[0]) + p[0], gelu_f(v[1]) + p[1], gelu_f(v[2]) + p[2], gelu_f(v[3]) + p[3]);
   } else if constexpr (EPI == EPI_HEADSPLIT) {
-    // l2 even: K -> [l2][slot][h][t][64]; l2 odd: V transposed -> [l2][slot][h][64][perm(t)]
-    // blocks padded to hs_T = TKP keys; perm: within each 32-key group, key 16*hi+4*g+j
-    // moves to 8*g+4*hi+j so a lane's 8 P.V keys are contiguous (k_cross_attn)
+    // l2 even: K -> [l2][slot][h][t][64]; l2 odd: V transposed, tile-major ->
+    // [l2][slot][h][t / 64][64 d][perm(t % 64)] (blocks of hs_T = TKP keys, a multiple of
+    // 64); perm: within each 32-key group, key 16*hi+4*g+j moves to 8*g+4*hi+j so a lane's
+    // 8 P.V keys are contiguous (k_cross_attn, k_xattn_seg)
     const int l2 = n / a.hs_state, c = n - l2 * a.hs_state, h = c >> 6, d = c & 63;
     const int64_t blk = (((int64_t)l2 * a.hs_nslots + a.hs_slot0 + gi) * a.hs_heads + h) * a.hs_T * 64;
     T* o = reinterpret_cast<T*>(a.out) + blk;
     if ((l2 & 1) == 0) {
       store4(o + (int64_t)ri * 64 + d, v[0], v[1], v[2], v[3]);
     } else {
-      const int q = ri & 31;
-      const int pt = (ri & ~31) + 8 * ((q & 15) >> 2) + 4 * (q >> 4) + (q & 3);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) o[(int64_t)(d + j) * a.hs_T + pt] = from_f32<T>(v[j]);
+      for (int j = 0; j < 4; ++j) o[xv_index(d + j, ri)] = from_f32<T>(v[j]);
     }
   } else if constexpr (EPI == EPI_QKV_ENC) {
     if (n < 2 * a.hs_state) {

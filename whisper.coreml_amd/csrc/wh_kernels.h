@@ -4,7 +4,8 @@
 
 namespace wh {
 
-constexpr int TKP = 1504;  // cross-KV keys per (window, head) block: 1500 padded to a multiple of 32
+constexpr int TKP = 1536;  // cross-KV keys per (window, head) block: 1500 padded to whole 64-key tiles
+// cross-V (V^T) is tile-major: xv_index (wh_common.h)
 
 template <typename T>
 void launch_layernorm(const float* x, T* y, const float* g, const float* b, int rows, int n, float eps,

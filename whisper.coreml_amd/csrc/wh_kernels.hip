@@ -160,7 +160,11 @@ __global__ __launch_bounds__(64 * ENC_NW) void k_attn_enc(const T* __restrict__ 
                                                   int64_t win_stride_in, const T* __restrict__ vt, int tkp,
                                                   T* __restrict__ out, int64_t win_stride_out) {
   constexpr int RT = ENC_RT, NT = 64 * ENC_NW;
-  constexpr int RS = 64 * (int)sizeof(T) + 16;  // LDS row stride (bytes)
+  // LDS row stride: 160 B for fp16 (40 dwords) makes the fragment reads (ds_read_b128,
+  // lane (r, g) at row r, 16 B chunk 2s + g) conflict-free in every 16-lane group of the
+  // instruction; the round-2 stride of 144 B gave 40 % extra LDS cycles
+  // (SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE, profiles/r03/enc_pmc.json)
+  constexpr int RS = 64 * (int)sizeof(T) + (sizeof(T) == 2 ? 32 : 16);
   __shared__ __attribute__((aligned(16))) char Ks[2][64 * RS];
   __shared__ __attribute__((aligned(16))) char Vt[2][64 * RS];
   const int h = blockIdx.y, w = blockIdx.z, H = gridDim.y;
@@ -677,7 +681,7 @@ void launch_reduce_store(const float* part, int nsplit, int64_t part_stride, con
 // Both MFMA operands load straight from HBM into fragments: K in its natural
 // [key][64] layout (A of S^T = K Q^T), V stored transposed [64][Tk] at encode time
 // (A of O^T = V^T P^T), so no LDS staging is needed; LDS only combines the NW waves.
-// ck: [win][head][TKP][64], cvt: [win][head][64][TKP] (key-permuted) for this layer.
+// ck: [win][head][TKP][64], cvt: [win][head] tile-major V^T (xv_index, wh_kernels.h) for this layer.
 // Partials per split: po[row][h][split][64], pm/pl[row][h][split] (k_cross_combine).
 // If qk_map != null the raw scores q.k of alignment heads are also written
 // (word timestamps, decoder.py:306-308): qk_out[(qk_map[h] * qk_rows + row) * Tk + key].
@@ -733,7 +737,7 @@ __global__ __launch_bounds__(64 * NW) void k_cross_attn(const T* __restrict__ q,
 #pragma unroll
   for (int dt = 0; dt < 4; ++dt)
 #pragma unroll
-    for (int s = 0; s < 2; ++s) frag_load(vf[dt][s], vbase + (int64_t)(dt * 16 + r) * TKP + ktl + 32 * s + 8 * g);
+    for (int s = 0; s < 2; ++s) frag_load(vf[dt][s], vbase + ((int64_t)(ktl >> 6) * 64 + dt * 16 + r) * 64 + 32 * s + 8 * g);
   if constexpr (QP) {
 #pragma unroll
     for (int z = 0; z < QZ; ++z) qv += pp[z];
@@ -878,8 +882,9 @@ __global__ __launch_bounds__(64) void k_cross_combine(const float* __restrict__ 
 // count re-arms it and merges every partial with sc1 loads (cdna_hip_programming.md §6
 // Guideline 16 R1, MI355X_MICROARCH.md "Valid forms").  RR: rows kept per partial in LDS
 // (8 when the beams are <= 8, else 16).
-// K: [slot][head][TKP][64]; V transposed [slot][head][64][TKP] with the 32-key
-// permutation, so both MFMA operands load straight from HBM into fragments.
+// K: [slot][head][TKP][64]; V transposed, tile-major (xv_index: a 64-key tile's 64 x 64
+// V^T is 8 KB contiguous, keys permuted within 32-key groups), so both MFMA operands load
+// straight from HBM into fragments and each tile is two contiguous 8 KB streams.
 constexpr float XS_LOG2E = 1.4426950408889634f;
 
 template <int RR>
@@ -948,7 +953,7 @@ __global__ __launch_bounds__(512, 1) void k_xattn_seg(const T* __restrict__ q, i
 #pragma unroll
     for (int dt = 0; dt < 4; ++dt)
 #pragma unroll
-      for (int s = 0; s < 2; ++s) frag_load_stream(vf[dt][s], vbase + (int64_t)(dt * 16 + r) * TKP + kt0 + 32 * s + 8 * g);
+      for (int s = 0; s < 2; ++s) frag_load_stream(vf[dt][s], vbase + ((int64_t)k * 64 + dt * 16 + r) * 64 + 32 * s + 8 * g);
   };
   // local tile i's softmax partial -> LDS slot i
   auto tile = [&](const Frag<T>(&kf)[4][2], const Frag<T>(&vf)[4][2], int i) {
@@ -1122,6 +1127,10 @@ int xattn_seg_grid(int npair, int nsp, int smax) {
   if (const char* e = tune_env("WHISPER_HIP_XS_K")) {
     const int v = atoi(e);
     if (v >= 1) k = v, forced = 1;
+    if (v < 0) {  // tuning: spread over min(-v, nseg) workgroups, uneven waves
+      const int nwg = std::min(-v, nseg);
+      return (nseg + nwg - 1) / nwg > smax ? (nseg + smax - 1) / smax : nwg;
+    }
   }
   if (!forced && npair >= 192) {
     const int ppw = (npair + 255) / 256, nwg = (npair + ppw - 1) / ppw;

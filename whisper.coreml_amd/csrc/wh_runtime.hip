@@ -696,11 +696,10 @@ struct Ctx : public wh_ctx {
       float* o = kv ? v : k;
       for (int hh = 0; hh < nh; ++hh)
         for (int t = 0; t < 1500; ++t) {
-          // K: [H][TKP][64]; V: transposed [H][64][TKP] with the 32-key permutation
-          const int q = t & 31, pt = (t & ~31) + 8 * ((q & 15) >> 2) + 4 * (q >> 4) + (q & 3);
+          // K: [H][TKP][64]; V: transposed, tile-major with the 32-key permutation (xv_index)
           for (int dd = 0; dd < 64; ++dd)
             o[((size_t)hh * 1500 + t) * 64 + dd] =
-                kv ? (float)h[((size_t)hh * 64 + dd) * TKP + pt] : (float)h[((size_t)hh * TKP + t) * 64 + dd];
+                kv ? (float)h[(size_t)hh * 64 * TKP + xv_index(dd, t)] : (float)h[((size_t)hh * TKP + t) * 64 + dd];
         }
     }
     return 0;
