@@ -394,23 +394,29 @@ __global__ __launch_bounds__(LP_THREADS) WH_LP_ATTR void k_logit_part(float* __r
   const int nseq = len - sb;
   const bool last_ts = nseq >= 1 && h1 >= tb, penult_ts = nseq < 2 || h2 >= tb, first = len == sb;
   const int ts_last = PM >= 0 ? PT : -1;
-  int mlo[4], mhi[4];
-  int nm = 0;
+  // the timestamp rules as four fixed [lo, hi) masks (unused: empty), no_ts and the blank
+  // tokens as four fixed ids (unused: -1): straight-line filter code per element
+  int mlo[4] = {0, 0, 0, 0}, mhi[4] = {0, 0, 0, 0};
+  int kid[5] = {-1, -1, -1, -1, -1};
   if (o.timestamps) {
     if (last_ts) {
-      if (penult_ts) { mlo[nm] = tb; mhi[nm++] = V; }
-      else { mlo[nm] = 0; mhi[nm++] = o.eot; }
+      if (penult_ts) { mlo[0] = tb; mhi[0] = V; }
+      else { mlo[0] = 0; mhi[0] = o.eot; }
     }
     if (ts_last >= 0) {
-      mlo[nm] = tb;
-      mhi[nm++] = (last_ts && !penult_ts) ? ts_last : ts_last + 1;
+      mlo[1] = tb;
+      mhi[1] = (last_ts && !penult_ts) ? ts_last : ts_last + 1;
     }
     if (first) {
-      mlo[nm] = 0; mhi[nm++] = tb;
-      if (o.max_initial >= 0) { mlo[nm] = tb + o.max_initial + 1; mhi[nm++] = V; }
+      mlo[2] = 0; mhi[2] = tb;
+      if (o.max_initial >= 0) { mlo[3] = tb + o.max_initial + 1; mhi[3] = V; }
     }
+    kid[4] = o.no_ts;
   }
-  const bool sb_first = first && o.suppress_blank;
+  if (first && o.suppress_blank)
+#pragma unroll
+    for (int b = 0; b < 4; ++b)
+      if (b < o.n_blank) kid[b] = o.blank[b];
   // 3. filters in place, then this wave's max and sum of exp (online rescale across waves)
   float mx = -INFINITY;
 #pragma unroll
@@ -418,12 +424,10 @@ __global__ __launch_bounds__(LP_THREADS) WH_LP_ATTR void k_logit_part(float* __r
     const int i = lo + tid + LP_THREADS * u;
     if (i >= hi) { xv[u] = -INFINITY; continue; }
     bool kill = (sw[u] >> (i & 31)) & 1u;
-    if (sb_first)
-      for (int b = 0; b < o.n_blank; ++b) kill |= (i == o.blank[b]);
-    if (o.timestamps) {
-      kill |= (i == o.no_ts);
-      for (int q = 0; q < nm; ++q) kill |= (i >= mlo[q] && i < mhi[q]);
-    }
+#pragma unroll
+    for (int b = 0; b < 5; ++b) kill |= i == kid[b];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) kill |= (i >= mlo[q] && i < mhi[q]);
     if (kill) {
       xv[u] = -INFINITY;
       row[i] = -INFINITY;
@@ -465,37 +469,22 @@ __global__ __launch_bounds__(LP_THREADS) WH_LP_ATTR void k_logit_part(float* __r
     const float gxw = own ? __shfl(myx, __ffsll((long long)own) - 1, 64) : -INFINITY;
     if (lane == 0) { wv_v[wv][0] = bv; wv_i[wv][0] = bi; wg_v[wv] = gv; wg_i[wv] = gi; wg_x[wv] = gxw; }
   } else {
-    // this wave's top-(G+1) by (value desc, index asc): per-lane insertion lists, then
-    // `need` wave-level argbest rounds
-    float lv[KC];
-    int li[KC];
-#pragma unroll
-    for (int q = 0; q < KC; ++q) { lv[q] = -INFINITY; li[q] = 0x7fffffff; }
-#pragma unroll
-    for (int u = 0; u < LP_EPT; ++u) {
-      const int i = lo + tid + LP_THREADS * u;
-      if (i >= hi) continue;
-      float v = xv[u];
-      int vi = i;
-#pragma unroll
-      for (int q = 0; q < KC; ++q) {
-        if (q < need && better(v, vi, lv[q], li[q])) {
-          const float tv = lv[q]; const int ti = li[q];
-          lv[q] = v; li[q] = vi; v = tv; vi = ti;
-        }
-      }
-    }
-    int head = 0;
+    // this wave's top-(G+1) by (value desc, index asc): `need` rounds of a wave-level
+    // argbest over every lane's best element not yet taken (bit u of `taken`: element u
+    // left the lane's candidates).  Same list as per-lane insertion lists merged head by
+    // head (the round-2 form, whose swap chains compiled to ~5k register moves per wave).
+    unsigned taken = 0u;
     for (int q = 0; q < need; ++q) {
-      float hv = -INFINITY;
-      int hix = 0x7fffffff;
+      float bv = -INFINITY;
+      int bi = 0x7fffffff;
 #pragma unroll
-      for (int z = 0; z < KC; ++z)
-        if (z == head) { hv = lv[z]; hix = li[z]; }
-      float bv = hv;
-      int bi = hix;
+      for (int u = 0; u < LP_EPT; ++u) {
+        const int i = lo + tid + LP_THREADS * u;
+        if (i < hi && !((taken >> u) & 1u) && better(xv[u], i, bv, bi)) { bv = xv[u]; bi = i; }
+      }
+      const int mine = bi;
       wave_argbest(bv, bi);
-      if (bi == hix && bi != 0x7fffffff) ++head;
+      if (mine == bi && bi != 0x7fffffff) taken |= 1u << ((bi - lo - tid) / LP_THREADS);
       if (lane == 0) { wv_v[wv][q] = bv; wv_i[wv][q] = bi; }
     }
   }

@@ -44,6 +44,7 @@ struct GemmArgs {
   const int* x_rows = nullptr;
   int ksplit = 1;
   int mt_block = 0;  // 16-row tiles per block (0 = min(ceil(M/16), 8))
+  int row_groups = 1;  // k_vocab_small: row groups (set by the launcher)
   // k_proj PRO_LN prologue: X = LayerNorm(xf32 rows; ln_g, ln_b, ln_eps)
   const float* xf32 = nullptr;
   const float* ln_g = nullptr;

@@ -423,14 +423,19 @@ __global__ __launch_bounds__(512) void k_gemv_rows(GemmArgs a) {
   }
 }
 
-// ============================================================ vocabulary projection, <= 32 rows
-// logits[m][n] = sum_k X[m][k] E[n][k] for a decoder step's few rows (one window's beams)
-// against the whole token embedding (V = 51866 columns, 133 MB in fp16).  X (<= 32 rows)
-// is staged in LDS once per workgroup; every WAVE then owns whole 16-column tiles (all of
-// K: no cross-wave reduction, no barrier in the loop), visiting tiles gw, gw + nwaves, ...
-// so the weight stream is split evenly over the chip's waves (12-13 tiles per CU).  Its
-// weight fragments stream in chunks of VC k-steps, the next chunk (of this tile or of the
-// wave's next tile) in flight while the current one is multiplied.
+// ============================================================ vocabulary projection
+// logits[m][n] = sum_k X[m][k] E[n][k] for a decoder step's rows against the whole token
+// embedding (V = 51866 columns, 133 MB in fp16).  The rows are cut into a.row_groups groups
+// of RG = ceil(M / row_groups) <= 64 rows, each small enough to sit in LDS with all of K
+// (fp16, K 1280: <= 60 rows; 100 rows = 2 groups of 50); a workgroup stages its group's
+// rows once, then every WAVE owns whole 16-column tiles (all of K: no cross-wave reduction,
+// no barrier in the loop), visiting tiles gw, gw + nwaves, ... so the weight stream is split
+// evenly over the group's waves.  Its weight fragments stream in chunks of VC k-steps, the
+// next chunk (of this tile or of the wave's next tile) in flight while the current one is
+// multiplied.  The groups of one column range are adjacent logical ids (xcd_remap: one
+// XCD), so the second group's weight reads mostly hit that XCD's L2.
+// Every output element is one row's dot product in a fixed k order: a row's logits do not
+// depend on the other rows or on the grouping (batch invariance).
 template <typename T, int MT>
 __global__ __launch_bounds__(512) void k_vocab_small(GemmArgs a) {
   constexpr int VC = 8;  // k-steps per chunk
@@ -438,6 +443,11 @@ __global__ __launch_bounds__(512) void k_vocab_small(GemmArgs a) {
   const int K = a.K, S = K / 32, nch = (S + VC - 1) / VC;
   const int xrow = K * (int)sizeof(T) + 16;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = lane & 15, g = lane >> 4;
+  // row group: rows [m0, m0 + RG) of X in LDS rows [0, RG); gridDim.y groups, adjacent ids
+  const int ngrp = a.row_groups, RG = (a.M + ngrp - 1) / ngrp;
+  const int lid = xcd_remap(blockIdx.x, gridDim.x);
+  const int grp = lid % ngrp, cblk = lid / ngrp, ncblk = gridDim.x / ngrp;
+  const int m0 = grp * RG;
   const T* X = reinterpret_cast<const T*>(a.X);
   const T* W = reinterpret_cast<const T*>(a.W);
   if (a.xf32) {
@@ -446,7 +456,7 @@ __global__ __launch_bounds__(512) void k_vocab_small(GemmArgs a) {
     // per row, two passes in registers (the arithmetic of k_layernorm / k_proj1)
     constexpr int CPLM = 5;  // float4 chunks per lane: K <= 1280
     const int CH = K / 4;
-    for (int row = wave; row < MT * 16; row += 8) {
+    for (int row = wave; row < RG; row += 8) {  // M <= 8: one group (launcher)
       T* dst = reinterpret_cast<T*>(xsv + row * xrow);
       if (row >= a.M) {
         for (int c = lane; c < CH; c += 64) store4(dst + 4 * c, 0.f, 0.f, 0.f, 0.f);
@@ -486,13 +496,13 @@ __global__ __launch_bounds__(512) void k_vocab_small(GemmArgs a) {
                  (v[3] - mean) * rstd * gv[i][3] + bv[i][3]);
         }
     }
-  } else {  // stage X rows (rows >= M: zeros)
-    const int cpr = K * (int)sizeof(T) / 16, total = MT * 16 * cpr;
+  } else {  // stage the group's X rows (rows >= M: zeros)
+    const int cpr = K * (int)sizeof(T) / 16, total = RG * cpr;
     for (int c = tid; c < total; c += 512) {
       const int row = c / cpr, col = c - row * cpr;
       float4_t v = (float4_t){0.f, 0.f, 0.f, 0.f};
-      if (row < a.M) {
-        const int xr = a.x_rows ? a.x_rows[row] : row;
+      if (m0 + row < a.M) {
+        const int xr = a.x_rows ? a.x_rows[m0 + row] : m0 + row;
         v = *reinterpret_cast<const float4_t*>(reinterpret_cast<const char*>(X + (int64_t)xr * a.ldx) + col * 16);
       }
       *reinterpret_cast<float4_t*>(xsv + row * xrow + col * 16) = v;
@@ -500,7 +510,7 @@ __global__ __launch_bounds__(512) void k_vocab_small(GemmArgs a) {
   }
   __syncthreads();
   const int nt = (a.N + 15) / 16;
-  const int gw = blockIdx.x * 8 + wave, nw = gridDim.x * 8;
+  const int gw = cblk * 8 + wave, nw = ncblk * 8;
   const int ntw = gw < nt ? (nt - 1 - gw) / nw + 1 : 0;  // tiles of this wave
   const int J = ntw * nch;                                 // chunks of this wave
   auto wsrc = [&](int j) {
@@ -534,7 +544,7 @@ __global__ __launch_bounds__(512) void k_vocab_small(GemmArgs a) {
 #pragma unroll
           for (int mt = 0; mt < MT; ++mt) {
             Frag<T> xf;
-            frag_load(xf, reinterpret_cast<const T*>(xsv + (mt * 16 + r) * xrow) + (s0 + c) * 32 + 8 * g);
+            frag_load(xf, reinterpret_cast<const T*>(xsv + min(mt * 16 + r, RG - 1) * xrow) + (s0 + c) * 32 + 8 * g);
             mfma_step(acc[mt], cur[c], xf);
           }
         }
@@ -543,8 +553,8 @@ __global__ __launch_bounds__(512) void k_vocab_small(GemmArgs a) {
         const int n = (gw + nw * (jj / nch)) * 16 + 4 * g;
 #pragma unroll
         for (int mt = 0; mt < MT; ++mt) {
-          const int m = mt * 16 + r;
-          if (m < a.M) {
+          const int m = m0 + mt * 16 + r;
+          if (mt * 16 + r < RG && m < a.M) {
 #if WH_WT
             const auto rs = wt_rsrc(a.out_f32);
 #pragma unroll
@@ -769,23 +779,33 @@ int launch_gemm_tiles(const GemmArgs& a, int epi, int tile_sel, hipStream_t st) 
     if (a.xf32 && !(vocab_small && epi == EPI_F32_COLS && a.N >= 16384 && a.M <= 8 && a.K <= 1280 && a.K % 32 == 0 &&
                     !a.x_rows))
       return -6;  // the LayerNorm prologue exists only in k_vocab_small
-    if (vocab_small && epi == EPI_F32_COLS && a.N >= 16384 && a.M <= (sizeof(T) == 2 ? 32 : 16) && a.K <= 1280 &&
-        a.K % 32 == 0) {
-      const int mtv = (a.M + 15) / 16;
-      const int lds = mtv * 16 * (a.K * (int)sizeof(T) + 16);
-      const int grid = std::min(256, (a.N + 127) / 128);
-      if (mtv == 1) {
-        static bool attr1 = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_vocab_small<T, 1>),
-                                                hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024) == hipSuccess;
-        if (!attr1) return -5;
-        k_vocab_small<T, 1><<<grid, 512, lds, st>>>(a);
-      } else {
-        static bool attr2 = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_vocab_small<T, 2>),
-                                                hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024) == hipSuccess;
-        if (!attr2) return -5;
-        k_vocab_small<T, 2><<<grid, 512, lds, st>>>(a);
+    // k_vocab_small: the rows in groups of <= 64 that fit LDS with all of K (152 KB)
+    const int vxrow = a.K * (int)sizeof(T) + 16;
+    const int vrg_max = std::min(64, (152 * 1024) / vxrow);
+    const int vgrp = (a.M + vrg_max - 1) / vrg_max;
+    // (<= 32 rows: at 100 rows, 2 groups of 50, it measured 89.2 us against k_gemv_x's 84.6:
+    // each CU streams its column block twice, profiles/r03/vocab_groups_ab.txt)
+    if (vocab_small && epi == EPI_F32_COLS && a.N >= 16384 && a.M <= (sizeof(T) == 2 ? 32 : 16) && vgrp <= 4 &&
+        a.K <= 1280 && a.K % 32 == 0) {
+      const int rg = (a.M + vgrp - 1) / vgrp, mtv = (rg + 15) / 16;
+      const int lds = rg * vxrow;
+      const int grid = vgrp * std::max(1, std::min(256 / vgrp, (a.N + 127) / 128));
+      GemmArgs av = a;
+      av.row_groups = vgrp;
+      auto go = [&](auto mtc) {  // one attribute flag per instantiation
+        constexpr int MTV = decltype(mtc)::value;
+        static bool attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_vocab_small<T, MTV>),
+                                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) == hipSuccess;
+        if (!attr) return -5;
+        k_vocab_small<T, MTV><<<grid, 512, lds, st>>>(av);
+        return 0;
+      };
+      switch (mtv) {
+        case 1: return go(std::integral_constant<int, 1>());
+        case 2: return go(std::integral_constant<int, 2>());
+        case 3: return go(std::integral_constant<int, 3>());
+        default: return go(std::integral_constant<int, 4>());
       }
-      return 0;
     }
     if (mt >= 3 && epi == EPI_F32_COLS && a.N >= 16384) {
       // vocabulary projection: NW column tiles share each staged X subchunk, so X
