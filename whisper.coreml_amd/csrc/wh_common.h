@@ -48,6 +48,13 @@ static inline const char* tune_env(const char* name) {
 // cross-V (V^T) of a (window, head) is TILE-MAJOR: [TKP / 64 tiles][64 d][64 keys, 32-key permutation],
 // so one 64-key tile's V^T is 8 KB contiguous (one stream, like K's [TKP][64] rows); element (d, t)
 // sits at xv_index(d, t).
+// 2^x as the bare v_exp_f32 (exp2f adds a denormal-range rescale: 5 more instructions per
+// call).  Softmax uses only: a result below 2^-126 is flushed instead of kept denormal,
+// which leaves every fp16 probability (min subnormal 2^-24) and every fp32 sum that
+// includes the row maximum's 1 unchanged.
+WH_DEV float hw_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
+typedef float f32x2_t __attribute__((ext_vector_type(2)));  // packed fp32 (v_pk_add_f32 / v_pk_mul_f32)
+
 WH_DEV_HOST int xv_perm(int t) {
   const int q = t & 31;
   return (t & ~31) + 8 * ((q & 15) >> 2) + 4 * (q >> 4) + (q & 3);

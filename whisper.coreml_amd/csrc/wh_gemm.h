@@ -127,6 +127,65 @@ WH_DEV void epilogue_store(const GemmArgs& a, int m, int gi, int ri, int n, floa
   }
 }
 
+// The epilogue of a tile whose lane holds acc[mi][ni] = Y[mrow(mi)][ncol(ni) .. +3]:
+// the bias of the lane's columns is loaded once (it depends on n only), and an epilogue
+// that reads memory per element (EPI_RESID: the residual x; EPI_GELU_POS: pos) issues
+// every such load of a group of MG row tiles before the group's first store.  Written as
+// one loop of epilogue_store calls, the compiler keeps each load behind the previous
+// store (they may alias) and waits on it at once: 2 x MI x NI dependent round trips per
+// tile (k_gemm_256 EPI_RESID: ~57 us of a 256 x 256 tile; profiles/r03/gemm_epilogue_ab.txt).
+// Same arithmetic as epilogue_store: v = acc (+ bias), then the epilogue's own op.
+template <typename T, int EPI, int MI, int NI, int MG, typename RowF, typename ColF>
+WH_DEV void tile_epilogue(const GemmArgs& a, const float4_t (&acc)[MI][NI], RowF mrow, ColF ncol) {
+  static_assert(MI % MG == 0, "row-tile groups");
+  constexpr bool LD = EPI == EPI_RESID || EPI == EPI_GELU_POS;
+  float4_t bv[NI];
+#pragma unroll
+  for (int ni = 0; ni < NI; ++ni) bv[ni] = a.bias ? load4f(a.bias + ncol(ni)) : (float4_t){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int g0 = 0; g0 < MI; g0 += MG) {
+    float4_t xv[LD ? MG : 1][LD ? NI : 1];
+    if constexpr (LD) {
+#pragma unroll
+      for (int j = 0; j < MG; ++j) {
+        const int m = mrow(g0 + j);
+        const int gi = m / a.x_group_rows, ri = m - gi * a.x_group_rows;
+#pragma unroll
+        for (int ni = 0; ni < NI; ++ni) {
+          xv[j][ni] = (float4_t){0.f, 0.f, 0.f, 0.f};
+          if (m < a.M) {
+            if constexpr (EPI == EPI_RESID) xv[j][ni] = load4f(a.out_f32 + (int64_t)m * a.ldo + ncol(ni));
+            else xv[j][ni] = load4f(a.pos + (int64_t)ri * a.N + ncol(ni));
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < MG; ++j) {
+      const int m = mrow(g0 + j);
+      if (m >= a.M) continue;
+      const int gi = m / a.x_group_rows, ri = m - gi * a.x_group_rows;
+#pragma unroll
+      for (int ni = 0; ni < NI; ++ni) {
+        const int n = ncol(ni);
+        float4_t v = acc[g0 + j][ni];
+        if (a.bias) v += bv[ni];
+        if constexpr (EPI == EPI_RESID) {
+          float4_t c = xv[j][ni];
+          c += v;
+          store4(a.out_f32 + (int64_t)m * a.ldo + n, c[0], c[1], c[2], c[3]);
+        } else if constexpr (EPI == EPI_GELU_POS) {
+          const float4_t p = xv[j][ni];
+          store4(a.out_f32 + (int64_t)m * a.ldo + n, gelu_f(v[0]) + p[0], gelu_f(v[1]) + p[1], gelu_f(v[2]) + p[2],
+                 gelu_f(v[3]) + p[3]);
+        } else {
+          epilogue_store<T, EPI>(a, m, gi, ri, n, v);
+        }
+      }
+    }
+  }
+}
+
 template <typename T>
 int launch_gemm(const GemmArgs& a, int epi, hipStream_t st);
 // launch_gemm with the large-M tile chosen explicitly: 256 = k_gemm_256 where the shape

@@ -130,22 +130,9 @@ __global__ __launch_bounds__(256, 2) void k_gemm_tile(GemmArgs a) {
   }
 
   // epilogue: lane holds Y[m = m0+wr*64+mi*16+r][n = n0+wc*TBN_/2+ni*16+4g .. +3]
-#pragma unroll
-  for (int mi = 0; mi < 4; ++mi) {
-    const int m = m0 + wr * 64 + mi * 16 + r;
-    if (m >= a.M) continue;
-    const int gi = m / a.x_group_rows, ri = m - gi * a.x_group_rows;
-#pragma unroll
-    for (int ni = 0; ni < NI; ++ni) {
-      const int n = n0 + wc * (TBN_ / 2) + ni * 16 + 4 * g;
-      float4_t v = acc[mi][ni];
-      if (a.bias) {
-        const float4_t b = load4f(a.bias + n);
-        v += b;
-      }
-      epilogue_store<T, EPI>(a, m, gi, ri, n, v);
-    }
-  }
+  tile_epilogue<T, EPI, 4, NI, 2>(
+      a, acc, [&](int mi) { return m0 + wr * 64 + mi * 16 + r; },
+      [&](int ni) { return n0 + wc * (TBN_ / 2) + ni * 16 + 4 * g; });
 }
 
 // ============================================================ 256x256 pipelined GEMM (fp16)
@@ -321,19 +308,9 @@ __global__ __launch_bounds__(512, 1) void k_gemm_256(GemmArgs a) {
   if (wr == 0) raw_barrier();
 
   // epilogue: lane holds Y[m = m0 + wr*128 + mi*16 + r][n = n0 + wc*64 + ni*16 + 4g .. +3]
-#pragma unroll
-  for (int mi = 0; mi < 8; ++mi) {
-    const int m = m0 + wr * 128 + mi * 16 + r;
-    if (m >= a.M) continue;
-    const int gi = m / a.x_group_rows, ri = m - gi * a.x_group_rows;
-#pragma unroll
-    for (int ni = 0; ni < 4; ++ni) {
-      const int n = n0 + wc * 64 + ni * 16 + 4 * g;
-      float4_t v = acc[mi][ni];
-      if (a.bias) v += load4f(a.bias + n);
-      epilogue_store<half_t, EPI>(a, m, gi, ri, n, v);
-    }
-  }
+  tile_epilogue<half_t, EPI, 8, 4, 4>(
+      a, acc, [&](int mi) { return m0 + wr * 128 + mi * 16 + r; },
+      [&](int ni) { return n0 + wc * 64 + ni * 16 + 4 * g; });
 }
 
 // ============================================================ skinny weight-streaming GEMM

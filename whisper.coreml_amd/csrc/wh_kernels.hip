@@ -242,38 +242,53 @@ __global__ __launch_bounds__(64 * ENC_NW) void k_attn_enc(const T* __restrict__ 
     float alpha[RT];
 #pragma unroll
     for (int t = 0; t < RT; ++t) {
-      // mask ragged last tile; row max over the 64 keys
+      // mask the ragged last tile (a uniform branch: every other tile is whole); row max
+      // over the 64 keys
+      if (kb * 64 + 64 > Tlen) {
+#pragma unroll
+        for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            if (kb * 64 + kt * 16 + 4 * g + j >= Tlen) sc[t][kt][j] = -INFINITY;
+      }
       float mx = -INFINITY;
 #pragma unroll
       for (int kt = 0; kt < 4; ++kt)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int key = kb * 64 + kt * 16 + 4 * g + j;
-          if (key >= Tlen) sc[t][kt][j] = -INFINITY;
-          mx = fmaxf(mx, sc[t][kt][j]);
-        }
+        for (int j = 0; j < 4; ++j) mx = fmaxf(mx, sc[t][kt][j]);
       mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
       mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
       const float m_new = fmaxf(m_run[t], mx);
-      alpha[t] = exp2f((m_run[t] - m_new) * LOG2E);
-      float ps = 0.f;
+      alpha[t] = hw_exp2((m_run[t] - m_new) * LOG2E);
+      // p = 2^(s log2e - m log2e): one fma per score; the row sum in pairs (packed adds)
+      const float mL = m_new * LOG2E;
+      f32x2_t ps2 = {0.f, 0.f};
 #pragma unroll
       for (int kt = 0; kt < 4; ++kt)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const float p = exp2f((sc[t][kt][j] - m_new) * LOG2E);
-          ps += p;
-          pf[t][kt >> 1].v[(kt & 1) * 4 + j] = from_f32<T>(p);
+        for (int j = 0; j < 4; j += 2) {
+          const float p0 = hw_exp2(__builtin_fmaf(sc[t][kt][j], LOG2E, -mL));
+          const float p1 = hw_exp2(__builtin_fmaf(sc[t][kt][j + 1], LOG2E, -mL));
+          ps2 += (f32x2_t){p0, p1};
+          pf[t][kt >> 1].v[(kt & 1) * 4 + j] = from_f32<T>(p0);
+          pf[t][kt >> 1].v[(kt & 1) * 4 + j + 1] = from_f32<T>(p1);
         }
+      float ps = ps2[0] + ps2[1];
       ps += __shfl_xor(ps, 16, 64);
       ps += __shfl_xor(ps, 32, 64);
       l_run[t] = l_run[t] * alpha[t] + ps;
       m_run[t] = m_new;
     }
+    // rescale the output only when some row's running max moved (alpha == 1 otherwise:
+    // after the first tiles the max mostly settles; a wave-uniform branch, exact either way)
+#pragma unroll
+    for (int t = 0; t < RT; ++t)
+      if (__any(alpha[t] != 1.f)) {
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt) acc_o[t][dt] *= alpha[t];
+      }
 #pragma unroll
     for (int dt = 0; dt < 4; ++dt) {
-#pragma unroll
-      for (int t = 0; t < RT; ++t) acc_o[t][dt] *= alpha[t];
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
         // lane (r, g): V^T[d = dt*16 + r][keys 32s + {4g..4g+3, 16+4g..16+4g+3}], which
@@ -788,7 +803,7 @@ __global__ __launch_bounds__(64 * NW) void k_cross_attn(const T* __restrict__ q,
       for (int kt = 0; kt < 4; ++kt)
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          const float p = exp2f((sc[kt][j] - m) * LOG2E);
+          const float p = hw_exp2((sc[kt][j] - m) * LOG2E);
           ps += p;
           pf[kt >> 1].v[(kt & 1) * 4 + j] = from_f32<T>(p);
         }
@@ -818,7 +833,7 @@ __global__ __launch_bounds__(64 * NW) void k_cross_attn(const T* __restrict__ q,
       float f[NW], L = 0.f;
 #pragma unroll
       for (int w = 0; w < NW; ++w) {
-        f[w] = red_m[w][qq] == -INFINITY ? 0.f : exp2f((red_m[w][qq] - M) * LOG2E);
+        f[w] = red_m[w][qq] == -INFINITY ? 0.f : hw_exp2((red_m[w][qq] - M) * LOG2E);
         L += f[w] * red_l[w][qq];
       }
       const int row = rt + qq;
@@ -910,7 +925,7 @@ WH_DEV float4_t xs_merge(int n, Get get) {
 #pragma unroll
   for (int k = 0; k < XS_NSP; ++k)
     if (k < n) {
-      const float f = mv[k] == -INFINITY ? 0.f : exp2f((mv[k] - M) * XS_LOG2E);
+      const float f = mv[k] == -INFINITY ? 0.f : hw_exp2((mv[k] - M) * XS_LOG2E);
       L = __builtin_fmaf(f, lv[k], L);
 #pragma unroll
       for (int e = 0; e < 4; ++e) acc[e] = __builtin_fmaf(f, ov[k][e], acc[e]);
@@ -984,7 +999,7 @@ __global__ __launch_bounds__(512, 1) void k_xattn_seg(const T* __restrict__ q, i
     for (int kt = 0; kt < 4; ++kt)
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        const float pv = exp2f((sc[kt][j] - mx) * XS_LOG2E);
+        const float pv = hw_exp2((sc[kt][j] - mx) * XS_LOG2E);
         ps += pv;
         pf[kt >> 1].v[(kt & 1) * 4 + j] = from_f32<T>(pv);
       }
