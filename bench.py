@@ -128,7 +128,7 @@ def load_traffic(kernel):
     """HBM bytes per launch of `kernel` from the committed PMC pass
     (profiles/<round>/traffic.json, written by profiles/pmc_traffic.py: FETCH_SIZE x2
     + WRITE_SIZE per the gfx950 correction of MI355X_MICROARCH.md), or None."""
-    for rnd in ("r02", "r01"):
+    for rnd in ("r03", "r02", "r01"):
         path = os.path.join(REPO, "profiles", rnd, "traffic.json")
         try:
             with open(path) as f:
@@ -357,6 +357,7 @@ def main():
         "roofline_cross_attn": {"bound": "hbm", "kernel": f"{kern['xattn']} ({n_win} windows x {args.beam} beams)",
                                 "achieved": round(gbs(xattn_bytes, xattn_ms), 1), "peak": HBM_PEAK_GBS,
                                 "frac": round(gbs(xattn_bytes, xattn_ms) / HBM_PEAK_GBS, 4),
+                                "traffic": load_traffic(kern["xattn"]),
                                 "bytes_per_launch": xattn_bytes, "ms_per_launch": round(xattn_ms, 5)},
         "roofline_step": {"bound": "hbm", "kernel": f"decoder step hipGraph ({n_win} windows x {args.beam} beams)",
                           "achieved": round(gbs(step_bytes, step_ms), 1), "peak": HBM_PEAK_GBS,
