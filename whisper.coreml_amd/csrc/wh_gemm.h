@@ -189,8 +189,9 @@ WH_DEV void tile_epilogue(const GemmArgs& a, const float4_t (&acc)[MI][NI], RowF
 template <typename T>
 int launch_gemm(const GemmArgs& a, int epi, hipStream_t st);
 // launch_gemm with the large-M tile chosen explicitly: 256 = k_gemm_256 where the shape
-// allows it, 128 = k_gemm_tile (128 x 64 tiles below 256 tiles), 129 = k_gemm_tile with
-// 128 x 128 tiles only (tools/gemm_bench A/B; launch_gemm uses 256 unless WHISPER_HIP_GEMM)
+// allows it, 257 = the same with v_mfma_f32_32x32x16_f16 (A/B), 128 = k_gemm_tile (128 x 64
+// tiles below 256 tiles), 129 = k_gemm_tile with 128 x 128 tiles only (tools/gemm_bench
+// A/B; launch_gemm uses 256 unless WHISPER_HIP_GEMM)
 template <typename T>
 int launch_gemm_tiles(const GemmArgs& a, int epi, int tile_sel, hipStream_t st);
 

@@ -179,7 +179,10 @@ WH_DEV void glds16(const char* src, char* lds) {
                                    (__attribute__((address_space(3))) void*)(lds), 16, 0, 0);
 }
 
-template <int EPI>
+// MF = 16: v_mfma_f32_16x16x32_f16 (16 per phase); MF = 32: v_mfma_f32_32x32x16_f16 (8 per
+// phase, same operand bytes from the same LDS image: a lane reads row l & 31 of a 32-row
+// block, 16 B chunk 2(s & 1) + (l >> 5) of k-step s), acc as 4 x 2 32x32 tiles per wave
+template <int EPI, int MF = 16>
 __global__ __launch_bounds__(512, 1) void k_gemm_256(GemmArgs a) {
   using namespace g256;
   __shared__ __attribute__((aligned(1024))) char smem[2 * BUF];  // the kernel's only LDS object
@@ -236,21 +239,68 @@ __global__ __launch_bounds__(512, 1) void k_gemm_256(GemmArgs a) {
       for (int ks = 0; ks < 2; ++ks) bf[j][ks].v = *reinterpret_cast<const half8_t*>(base + (j * 2 + ks) * 1024);
   };
 
-  float4_t acc[8][4];
+  // 32x32x16 fragments: X (m) side af32[t][s] for the h-half's two 32-row tiles, W (n)
+  // side bf32[s] for the h-half's 32 columns, s = the four 16-deep k-steps of a K-tile
+  const int rr = lane & 15, hb = (lane >> 4) & 1, kh = lane >> 5;
+  const int coff0 = rr * 64 + (((0 + kh) ^ ((rr >> 3) << 1)) << 4);  // k-steps 0, 2
+  const int coff1 = rr * 64 + (((2 + kh) ^ ((rr >> 3) << 1)) << 4);  // k-steps 1, 3
+  Frag<half_t> af32[MF == 32 ? 2 : 1][4], bf32[4];
+  auto read_a32 = [&](int buf, int h) {
+    const char* base = smem + buf * BUF + (SA0 + h) * STAGE + wr * 8192;
 #pragma unroll
-  for (int i = 0; i < 8; ++i)
+    for (int t = 0; t < 2; ++t)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = (float4_t){0.f, 0.f, 0.f, 0.f};
+      for (int st = 0; st < 4; ++st)
+        af32[t][st].v = *reinterpret_cast<const half8_t*>(base + ((t * 2 + hb) * 2 + (st >> 1)) * 1024 +
+                                                             ((st & 1) ? coff1 : coff0));
+  };
+  auto read_b32 = [&](int buf, int h) {
+    const char* base = smem + buf * BUF + (SB0 + h) * STAGE + wc * 4096;
+#pragma unroll
+    for (int st = 0; st < 4; ++st)
+      bf32[st].v = *reinterpret_cast<const half8_t*>(base + (hb * 2 + (st >> 1)) * 1024 + ((st & 1) ? coff1 : coff0));
+  };
+  typedef float f32x16_t __attribute__((ext_vector_type(16)));
+  f32x16_t acc32[MF == 32 ? 4 : 1][2];
+  float4_t acc[MF == 32 ? 1 : 8][4];
+  if constexpr (MF == 32) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) acc32[i][j] = (f32x16_t){};
+  } else {
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = (float4_t){0.f, 0.f, 0.f, 0.f};
+  }
+  auto rd_a = [&](int buf, int h) {
+    if constexpr (MF == 32) read_a32(buf, h);
+    else read_a(buf, h);
+  };
+  auto rd_b = [&](int buf, int h) {
+    if constexpr (MF == 32) read_b32(buf, h);
+    else read_b(buf, h);
+  };
 
   auto mfma_quadrant = [&](int mh, int nh) {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_setprio(1);
+    if constexpr (MF == 32) {
 #pragma unroll
-    for (int mi = 0; mi < 4; ++mi)
+      for (int t = 0; t < 2; ++t)
 #pragma unroll
-      for (int j = 0; j < 2; ++j)
+        for (int st = 0; st < 4; ++st)
+          acc32[mh * 2 + t][nh] =
+              __builtin_amdgcn_mfma_f32_32x32x16_f16(bf32[st].v, af32[t][st].v, acc32[mh * 2 + t][nh], 0, 0, 0);
+    } else {
 #pragma unroll
-        for (int ks = 0; ks < 2; ++ks) mfma_step(acc[mh * 4 + mi][nh * 2 + j], bf[j][ks], af[mi][ks]);
+      for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+          for (int ks = 0; ks < 2; ++ks) mfma_step(acc[mh * 4 + mi][nh * 2 + j], bf[j][ks], af[mi][ks]);
+    }
     __builtin_amdgcn_s_setprio(0);
   };
 
@@ -260,26 +310,26 @@ __global__ __launch_bounds__(512, 1) void k_gemm_256(GemmArgs a) {
     constexpr int buf = decltype(bufc)::value;
     const bool s1 = t + 1 < nk, s2 = t + 2 < nk;
     // q0: Q(0,0)
-    read_b(buf, 0);
-    read_a(buf, 0);
+    rd_b(buf, 0);
+    rd_a(buf, 0);
     if (s1) stage(buf ^ 1, SA1, t + 1);
     raw_barrier();
     mfma_quadrant(0, 0);
     raw_barrier();
     // q1: Q(0,1)
-    read_b(buf, 1);
+    rd_b(buf, 1);
     if (s1) stage(buf ^ 1, SB0, t + 1);
     raw_barrier();
     mfma_quadrant(0, 1);
     raw_barrier();
     // q2: Q(1,1)
-    read_a(buf, 1);
+    rd_a(buf, 1);
     if (s2) stage(buf, SA0, t + 2);
     raw_barrier();
     mfma_quadrant(1, 1);
     raw_barrier();
     // q3: Q(1,0); retire tile t+1 before the barrier
-    read_b(buf, 0);
+    rd_b(buf, 0);
     if (s2) {
       stage(buf, SB1, t + 2);
       asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
@@ -307,10 +357,27 @@ __global__ __launch_bounds__(512, 1) void k_gemm_256(GemmArgs a) {
   }
   if (wr == 0) raw_barrier();
 
-  // epilogue: lane holds Y[m = m0 + wr*128 + mi*16 + r][n = n0 + wc*64 + ni*16 + 4g .. +3]
-  tile_epilogue<half_t, EPI, 8, 4, 4>(
-      a, acc, [&](int mi) { return m0 + wr * 128 + mi * 16 + r; },
-      [&](int ni) { return n0 + wc * 64 + ni * 16 + 4 * g; });
+  if constexpr (MF == 32) {
+    // lane holds, per 32x32 tile (mt, nt): m = m0 + wr*128 + mt*32 + (l & 31), n = n0 + wc*64 +
+    // nt*32 + 8q + 4(l >> 5) .. +3 in registers 4q .. 4q+3 (q = 0..3)
+    float4_t a4[4][8];
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int nt = j >> 2, q = j & 3;
+        a4[mt][j] = (float4_t){acc32[mt][nt][4 * q], acc32[mt][nt][4 * q + 1], acc32[mt][nt][4 * q + 2],
+                               acc32[mt][nt][4 * q + 3]};
+      }
+    tile_epilogue<half_t, EPI, 4, 8, 2>(
+        a, a4, [&](int mt) { return m0 + wr * 128 + mt * 32 + (lane & 31); },
+        [&](int j) { return n0 + wc * 64 + (j >> 2) * 32 + 8 * (j & 3) + 4 * kh; });
+  } else {
+    // lane holds Y[m = m0 + wr*128 + mi*16 + r][n = n0 + wc*64 + ni*16 + 4g .. +3]
+    tile_epilogue<half_t, EPI, 8, 4, 4>(
+        a, acc, [&](int mi) { return m0 + wr * 128 + mi * 16 + r; },
+        [&](int ni) { return n0 + wc * 64 + ni * 16 + 4 * g; });
+  }
 }
 
 // ============================================================ skinny weight-streaming GEMM
@@ -712,7 +779,7 @@ int launch_gemm_tiles(const GemmArgs& a, int epi, int tile_sel, hipStream_t st) 
   if (a.M <= 0) return 0;
   const bool big = a.M > 128 && (a.N % TBN) == 0 && (a.K % (TKB / (int)sizeof(T))) == 0 && epi != EPI_F32_COLS &&
                    epi != EPI_PARTIAL && a.x_rows == nullptr;
-  const bool t256 = big && sizeof(T) == 2 && tile_sel == 256 && a.M >= 256 && (a.N % g256::BN) == 0 &&
+  const bool t256 = big && sizeof(T) == 2 && (tile_sel == 256 || tile_sel == 257) && a.M >= 256 && (a.N % g256::BN) == 0 &&
                     (a.K % (2 * g256::BK)) == 0 && epi != EPI_QKV_DEC &&
                     // below one 256-tile per CU the 128-tile grid fills the chip better
                     // (tools/gemm_bench: one window, fc1: 0.035 vs 0.039 ms)
@@ -720,7 +787,11 @@ int launch_gemm_tiles(const GemmArgs& a, int epi, int tile_sel, hipStream_t st) 
   if (t256) {
     const int nwg = ((a.M + g256::BM - 1) / g256::BM) * (a.N / g256::BN);
     switch (epi) {
-#define CASE(E) case E: k_gemm_256<E><<<nwg, 512, 0, st>>>(a); break;
+#define CASE(E)                                                   \
+  case E:                                                         \
+    if (tile_sel == 257) k_gemm_256<E, 32><<<nwg, 512, 0, st>>>(a); \
+    else k_gemm_256<E><<<nwg, 512, 0, st>>>(a);                    \
+    break;
       CASE(EPI_STORE) CASE(EPI_STORE_GELU) CASE(EPI_RESID) CASE(EPI_GELU_POS) CASE(EPI_HEADSPLIT) CASE(EPI_QKV_ENC)
 #undef CASE
       default: return -1;

@@ -47,6 +47,9 @@ static double host_dot(const std::vector<half_t>& X, const std::vector<half_t>& 
 int main(int argc, char** argv) {
   const int nwin = argc > 1 ? atoi(argv[1]) : 20;
   const int rounds = argc > 2 ? atoi(argv[2]) : 7;
+  // the two launch_gemm_tiles selections compared (A, B): default 129 (k_gemm_tile 128x128)
+  // against 256 (the launcher); 256 257 compares the 16x16x32 and 32x32x16 MFMA forms
+  const int selA = argc > 3 ? atoi(argv[3]) : 129, selB = argc > 4 ? atoi(argv[4]) : 256;
   const int M = 1500 * nwin;
   const Shape shapes[] = {
       {"qkv", M, 3840, 1280, 1500, 0}, {"out", M, 1280, 1280, 1500, 0}, {"fc1", M, 5120, 1280, 1500, 0},
@@ -93,7 +96,7 @@ int main(int argc, char** argv) {
     a1.out = Y1;
     CK(hipMemset(Y0, 0, (size_t)s.M * s.N * 2));
     CK(hipMemset(Y1, 0, (size_t)s.M * s.N * 2));
-    if (launch_gemm_tiles<half_t>(a0, EPI_STORE, 129, 0) || launch_gemm_tiles<half_t>(a1, EPI_STORE, 256, 0)) {
+    if (launch_gemm_tiles<half_t>(a0, EPI_STORE, selA, 0) || launch_gemm_tiles<half_t>(a1, EPI_STORE, selB, 0)) {
       printf("%s: launch refused\n", s.name);
       return 1;
     }
@@ -123,7 +126,7 @@ int main(int argc, char** argv) {
     std::vector<float> t128, t256;
     for (int rd = 0; rd < rounds; ++rd) {
       for (int v = 0; v < 2; ++v) {
-        const int tile = v ? 256 : 129;
+        const int tile = v ? selB : selA;
         GemmArgs& av = v ? a1 : a0;
         launch_gemm_tiles<half_t>(av, EPI_STORE, tile, 0);
         CK(hipEventRecord(e0, 0));
@@ -139,9 +142,9 @@ int main(int argc, char** argv) {
     std::sort(t256.begin(), t256.end());
     const double fl = 2.0 * s.M * s.N * s.K;
     const float m128 = t128[t128.size() / 2], m256 = t256[t256.size() / 2];
-    printf("%-10s M=%6d N=%5d K=%5d  128: %.4f ms %6.1f TF | 256: %.4f ms %6.1f TF (min %.4f)  x%.2f | "
-           "max|256-128|/max|y| %.2e, max|256-fp64|/max|y| %.2e %s\n",
-           s.name, s.M, s.N, s.K, m128, fl / m128 / 1e9, m256, fl / m256 / 1e9, t256[0], m128 / m256, dmax / ymax,
+    printf("%-10s M=%6d N=%5d K=%5d  %d: %.4f ms %6.1f TF | %d: %.4f ms %6.1f TF (min %.4f)  x%.2f | "
+           "max|B-A|/max|y| %.2e, max|B-fp64|/max|y| %.2e %s\n",
+           s.name, s.M, s.N, s.K, selA, m128, fl / m128 / 1e9, selB, m256, fl / m256 / 1e9, t256[0], m128 / m256, dmax / ymax,
            emax, ok ? "ok" : "FAIL");
     fflush(stdout);
     CK(hipFree(X));
