@@ -317,7 +317,11 @@ def main():
     def gbs(b, ms):
         return b / (ms * 1e-3) / 1e9
 
-    traffic = load_traffic(kern["proj"])
+    # the committed PMC pass (profiles/pmc_traffic.py) ran large-v3 at 20 windows (k_proj,
+    # k_xattn_seg) and at one window (k_proj1): other shapes report no traffic
+    lv3 = args.model == "large-v3"
+    traffic = load_traffic(kern["proj"]) if lv3 and (p1 or n_win == 20) else None
+    xattn_traffic = load_traffic(kern["xattn"]) if lv3 and n_win == 20 else None
     parallel = (f"one {file_seconds:.0f} s file sharded over {world} GPU(s) by 30 s clips (whisper/distributed.py): "
                 f"RCCL all-reduce(max) of the log-mel maximum + gather of the segment records")
     out = {
@@ -357,7 +361,7 @@ def main():
         "roofline_cross_attn": {"bound": "hbm", "kernel": f"{kern['xattn']} ({n_win} windows x {args.beam} beams)",
                                 "achieved": round(gbs(xattn_bytes, xattn_ms), 1), "peak": HBM_PEAK_GBS,
                                 "frac": round(gbs(xattn_bytes, xattn_ms) / HBM_PEAK_GBS, 4),
-                                "traffic": load_traffic(kern["xattn"]),
+                                "traffic": xattn_traffic,
                                 "bytes_per_launch": xattn_bytes, "ms_per_launch": round(xattn_ms, 5)},
         "roofline_step": {"bound": "hbm", "kernel": f"decoder step hipGraph ({n_win} windows x {args.beam} beams)",
                           "achieved": round(gbs(step_bytes, step_ms), 1), "peak": HBM_PEAK_GBS,

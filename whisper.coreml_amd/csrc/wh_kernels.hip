@@ -152,14 +152,17 @@ void launch_resid_ln(float* x, const float* part, int nsplit, int64_t part_strid
 // Block = ENC_NW waves x ENC_RT row tiles of 16 queries; each K / V fragment read from
 // LDS feeds ENC_RT MFMAs.  S^T = K Q^T and O^T = V^T P^T so each lane owns one query row per row tile
 // (see wh_common.h).
-constexpr int ENC_RT = 1;  // query row tiles per wave (2 measured 414 us vs 289: 264 VGPRs, one block per CU)
+// query row tiles per wave: 2 measured 414 vs 289 us in round 2 (264 VGPRs, one block per
+// CU) and, after the round-3 VALU trims (134 VGPRs), 3.60 vs 3.45 ms per encoder window
+// (profiles/r03/enc_rt_ab.txt)
+constexpr int ENC_RT = 1;
 // ENC_NW waves per block: the K/V tile staged once for 16 * ENC_NW * ENC_RT queries; 8,
 // or 4 when 8-wave blocks would give fewer than two per CU (one window: 240 -> 480 blocks)
-template <typename T, int ENC_NW>
+template <typename T, int ENC_NW, int RT = ENC_RT>
 __global__ __launch_bounds__(64 * ENC_NW) void k_attn_enc(const T* __restrict__ qkv, int ld, int ns, int Tlen,
                                                   int64_t win_stride_in, const T* __restrict__ vt, int tkp,
                                                   T* __restrict__ out, int64_t win_stride_out) {
-  constexpr int RT = ENC_RT, NT = 64 * ENC_NW;
+  constexpr int NT = 64 * ENC_NW;
   // LDS row stride: 160 B for fp16 (40 dwords) makes the fragment reads (ds_read_b128,
   // lane (r, g) at row r, 16 B chunk 2s + g) conflict-free in every 16-lane group of the
   // instruction; the round-2 stride of 144 B gave 40 % extra LDS cycles
