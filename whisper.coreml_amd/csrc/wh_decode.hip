@@ -344,12 +344,15 @@ __device__ __forceinline__ void wave_argbest(float& v, int& idx) {
   }
 }
 
+template <int NS>
+__device__ __forceinline__ void lp_combine(const LPRec* rec, int r, const DecState& s, const DecOpts& o, int lane);
+
 // Two barriers per workgroup: (1) after the history scan (last sampled timestamp), (2)
 // after every wave has reduced its own max, rescaled sum of exp and top-(G+1) list (or
 // argbest / Gumbel best); wave 0 then merges the 8 wave results and writes the record.
 // The slice's logits and suppress words are loaded first, before the history, so their
 // round trip overlaps it.
-template <int NS, int LP_EPT>
+template <int NS, int LP_EPT, bool FUSED>
 __global__ __launch_bounds__(LP_THREADS) WH_LP_ATTR void k_logit_part(float* __restrict__ logits, int ldl, DecState s,
                                                            DecOpts o) {
   constexpr int NWV = LP_THREADS / 64;
@@ -442,7 +445,34 @@ __global__ __launch_bounds__(LP_THREADS) WH_LP_ATTR void k_logit_part(float* __r
   }
   se = wave_sum(se);
   if (lane == 0) { wmx[wv] = mx; wse[wv] = se; }
-  LPRec* rec = reinterpret_cast<LPRec*>(s.lpart + ((int64_t)r * LP_SLICES + j) * LP_REC);  // NS <= LP_SLICES
+  // this slice's record, stored write-through (sc1) by lane 0 of wave 0 (NS <= LP_SLICES)
+  const auto rrs = wt_rsrc(s.lpart + (int64_t)r * LP_SLICES * LP_REC);
+  const int rec_off = j * LP_REC * 4;
+  auto wt_rec = [&](int off, float v) { wt_store1(rrs, off, v); };
+  // FUSED: the row's last slice to finish merges all NS records (the k_logit_combine
+  // launch folded in; cdna_hip_programming.md §6 Guideline 16 R1, as k_xattn_seg): the
+  // record's sc1 stores drained (vmcnt(0)), a relaxed agent add on the row's counter; the
+  // wave drawing NS - 1 re-arms it and reads the NS records with sc1 loads into LDS
+  __shared__ __attribute__((aligned(16))) float recs[FUSED ? NS * LP_REC : 4];
+  auto arrive_and_combine = [&]() {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    int ticket = 0;
+    if (lane == 0) ticket = __hip_atomic_fetch_add(s.lp_cnt + r, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    ticket = __shfl(ticket, 0, 64);
+    if (ticket != NS - 1) return;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // no instruction: keeps the loads below the add
+    if (lane == 0) __hip_atomic_store(s.lp_cnt + r, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    constexpr int N4 = NS * LP_REC / 4, PER = (N4 + 63) / 64;
+    float4_t v[PER];
+#pragma unroll
+    for (int k = 0; k < PER; ++k)
+      v[k] = __builtin_bit_cast(float4_t, __builtin_amdgcn_raw_buffer_load_b128(rrs, min(lane + 64 * k, N4 - 1) * 16, 0, 16));
+#pragma unroll
+    for (int k = 0; k < PER; ++k)
+      if (lane + 64 * k < N4) reinterpret_cast<float4_t*>(recs)[lane + 64 * k] = v[k];
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // one wave: its own LDS writes, no barrier
+    lp_combine<NS>(reinterpret_cast<const LPRec*>(recs), r, s, o, lane);
+  };
   const int need = s.G + 1;
   if (!o.beam) {
     float bv = -INFINITY, gv = -INFINITY, gx = -INFINITY;
@@ -510,9 +540,12 @@ __global__ __launch_bounds__(LP_THREADS) WH_LP_ATTR void k_logit_part(float* __r
     const unsigned long long own = __ballot(mine == gi && gi != 0x7fffffff);
     const float gx = own ? __shfl(myx, __ffsll((long long)own) - 1, 64) : -INFINITY;
     if (lane == 0) {
-      rec->mx = MX; rec->se = SE; rec->bv = bv; rec->bi = bi;
-      rec->gv = gv; rec->gi = gi; rec->gx = gi != 0x7fffffff ? gx : -INFINITY;
+      wt_rec(rec_off + offsetof(LPRec, mx), MX); wt_rec(rec_off + offsetof(LPRec, se), SE);
+      wt_rec(rec_off + offsetof(LPRec, bv), bv); wt_rec(rec_off + offsetof(LPRec, bi), __builtin_bit_cast(float, bi));
+      wt_rec(rec_off + offsetof(LPRec, gv), gv); wt_rec(rec_off + offsetof(LPRec, gi), __builtin_bit_cast(float, gi));
+      wt_rec(rec_off + offsetof(LPRec, gx), gi != 0x7fffffff ? gx : -INFINITY);
     }
+    if constexpr (FUSED) arrive_and_combine();
     return;
   }
   // beam: each lane holds up to two wave candidates (NWV * need <= 72), sorted within
@@ -531,32 +564,20 @@ __global__ __launch_bounds__(LP_THREADS) WH_LP_ATTR void k_logit_part(float* __r
     int bi = i0;
     wave_argbest(bv, bi);
     if (bi == i0 && bi != 0x7fffffff) { a0 = a1; i0 = i1; a1 = -INFINITY; i1 = 0x7fffffff; }
-    if (lane == 0) { rec->tv[q] = bv; rec->ti[q] = bi; }
+    if (lane == 0) {
+      wt_rec(rec_off + offsetof(LPRec, tv) + 4 * q, bv);
+      wt_rec(rec_off + offsetof(LPRec, ti) + 4 * q, __builtin_bit_cast(float, bi));
+    }
   }
-  if (lane == 0) { rec->mx = MX; rec->se = SE; }
+  if (lane == 0) { wt_rec(rec_off + offsetof(LPRec, mx), MX); wt_rec(rec_off + offsetof(LPRec, se), SE); }
+  if constexpr (FUSED) arrive_and_combine();
 }
 
+// the merge of a row's NS slice records (in LDS, `rec`) by one wave: the timestamp-rule
+// selection between text and timestamps, the normaliser, then argbest / top-(G+1) with one
+// slice per lane (decoding.py:522-531 and the candidate lists of 707-733)
 template <int NS>
-__global__ __launch_bounds__(64) void k_logit_combine(DecState s, DecOpts o) {
-  const int r = blockIdx.x, w = r / s.G, lane = threadIdx.x;
-  // the row's slice records -> LDS in one round trip, issued with the done flag's load
-  // (the merge below reads them serially; from global memory every read would be a
-  // dependent load)
-  __shared__ __attribute__((aligned(16))) float recs[NS * LP_REC];
-  {
-    constexpr int N4 = NS * LP_REC / 4, PER = (N4 + 63) / 64;
-    const float4_t* src = reinterpret_cast<const float4_t*>(s.lpart + (int64_t)r * LP_SLICES * LP_REC);
-    float4_t* dst = reinterpret_cast<float4_t*>(recs);
-    float4_t v[PER];
-#pragma unroll
-    for (int k = 0; k < PER; ++k) v[k] = src[min(lane + 64 * k, N4 - 1)];
-    if (s.done[w]) return;
-#pragma unroll
-    for (int k = 0; k < PER; ++k)
-      if (lane + 64 * k < N4) dst[lane + 64 * k] = v[k];
-  }
-  __syncthreads();
-  const LPRec* rec = reinterpret_cast<const LPRec*>(recs);
+__device__ __forceinline__ void lp_combine(const LPRec* rec, int r, const DecState& s, const DecOpts& o, int lane) {
   constexpr int TS = NS - 1;
   float m = -INFINITY;
   for (int j = 0; j < NS; ++j) m = fmaxf(m, rec[j].mx);
@@ -621,6 +642,28 @@ __global__ __launch_bounds__(64) void k_logit_combine(DecState s, DecOpts o) {
   }
 }
 
+template <int NS>
+__global__ __launch_bounds__(64) void k_logit_combine(DecState s, DecOpts o) {
+  const int r = blockIdx.x, w = r / s.G, lane = threadIdx.x;
+  // the row's slice records -> LDS in one round trip, issued with the done flag's load
+  // (the merge reads them serially; from global memory every read would be a dependent load)
+  __shared__ __attribute__((aligned(16))) float recs[NS * LP_REC];
+  {
+    constexpr int N4 = NS * LP_REC / 4, PER = (N4 + 63) / 64;
+    const float4_t* src = reinterpret_cast<const float4_t*>(s.lpart + (int64_t)r * LP_SLICES * LP_REC);
+    float4_t* dst = reinterpret_cast<float4_t*>(recs);
+    float4_t v[PER];
+#pragma unroll
+    for (int k = 0; k < PER; ++k) v[k] = src[min(lane + 64 * k, N4 - 1)];
+    if (s.done[w]) return;
+#pragma unroll
+    for (int k = 0; k < PER; ++k)
+      if (lane + 64 * k < N4) dst[lane + 64 * k] = v[k];
+  }
+  __syncthreads();
+  lp_combine<NS>(reinterpret_cast<const LPRec*>(recs), r, s, o, lane);
+}
+
 void launch_logit_rows(float* logits, int ldl, const DecState& s, const DecOpts& o, int nwin, hipStream_t st) {
   // the sliced selection (k_logit_part + k_logit_combine) unless WHISPER_HIP_LOGIT_SPLIT=0
   // (config 2, turbo one window: 0.380 -> 0.346 ms per token; config 3 unchanged)
@@ -629,14 +672,26 @@ void launch_logit_rows(float* logits, int ldl, const DecState& s, const DecOpts&
     return !(e && e[0] == '0');
   }();
   const int rows = nwin * s.G;
+  // the records merged by the row's last slice (fused) unless WHISPER_HIP_LP_FUSED=0 (tuning:
+  // k_logit_combine as its own launch)
+  const char* fe = tune_env("WHISPER_HIP_LP_FUSED");
+  const bool fused = !(fe && fe[0] == '0');
   if (split && o.ts_begin > 0 && rows <= 32 && (o.ts_begin + 30) / 31 <= LP_THREADS * 4 && o.V - o.ts_begin <= LP_THREADS * 4) {
-    k_logit_part<32, 4><<<dim3(rows, 32), LP_THREADS, 0, st>>>(logits, ldl, s, o);
-    k_logit_combine<32><<<rows, 64, 0, st>>>(s, o);
+    if (fused) {
+      k_logit_part<32, 4, true><<<dim3(rows, 32), LP_THREADS, 0, st>>>(logits, ldl, s, o);
+    } else {
+      k_logit_part<32, 4, false><<<dim3(rows, 32), LP_THREADS, 0, st>>>(logits, ldl, s, o);
+      k_logit_combine<32><<<rows, 64, 0, st>>>(s, o);
+    }
     return;
   }
   if (split && o.ts_begin > 0 && (o.ts_begin + 6) / 7 <= LP_THREADS * 16 && o.V - o.ts_begin <= LP_THREADS * 16) {
-    k_logit_part<8, 16><<<dim3(rows, 8), LP_THREADS, 0, st>>>(logits, ldl, s, o);
-    k_logit_combine<8><<<rows, 64, 0, st>>>(s, o);
+    if (fused) {
+      k_logit_part<8, 16, true><<<dim3(rows, 8), LP_THREADS, 0, st>>>(logits, ldl, s, o);
+    } else {
+      k_logit_part<8, 16, false><<<dim3(rows, 8), LP_THREADS, 0, st>>>(logits, ldl, s, o);
+      k_logit_combine<8><<<rows, 64, 0, st>>>(s, o);
+    }
     return;
   }
   k_logit_rows<<<nwin * s.G, LR_THREADS, 0, st>>>(logits, ldl, s, o);

@@ -86,6 +86,7 @@ struct DecState {
   float* cand_val;   // [nw*G][KC]
   int* cand_idx;     // [nw*G][KC]
   float* lpart;      // [nw*G][LP_SLICES][LP_REC] per-slice token-selection partials
+  int* lp_cnt;       // [nw*G] slice arrival counters of k_logit_part (zero between launches)
   unsigned long long* seed;  // [1] sampling seed (device memory: not part of a captured graph)
   int nw, G, ctx, hctx, maxc;
 };

@@ -328,7 +328,7 @@ struct Ctx : public wh_ctx {
     addA(Wcap * Gcap * 4);
     addA(Wcap * 16 * 4); addA(Wcap * 16 * 4); addA((size_t)Wcap * 16 * HCTX * 4);
     addA((size_t)Wcap * Gcap * KC * 4); addA((size_t)Wcap * Gcap * KC * 4);
-    addA((size_t)Wcap * Gcap * LP_SLICES * LP_REC * 4);
+    addA((size_t)Wcap * Gcap * LP_SLICES * LP_REC * 4); addA((size_t)Wcap * Gcap * 4);
     addA(64);
     addA(64);
     addA((size_t)P1_SLABS * 256 * 4); addA((size_t)(4 * n / 16) * 4);  // k_proj1 split-K slabs + counters
@@ -364,12 +364,12 @@ struct Ctx : public wh_ctx {
     S.sum_lp = fa(Wcap * Gcap);
     S.fin_score = fa(Wcap * 16); S.fin_len = ia(Wcap * 16); S.fin_tok = ia((size_t)Wcap * 16 * HCTX);
     S.cand_val = fa((size_t)Wcap * Gcap * KC); S.cand_idx = ia((size_t)Wcap * Gcap * KC);
-    S.lpart = fa((size_t)Wcap * Gcap * LP_SLICES * LP_REC);
+    S.lpart = fa((size_t)Wcap * Gcap * LP_SLICES * LP_REC); S.lp_cnt = ia((size_t)Wcap * Gcap);  // zeroed with the arena
     S.seed = (unsigned long long*)aa.take(64);
     p1_slab = fa((size_t)P1_SLABS * 256); p1_cnt = ia(4 * n / 16);  // zeroed with the arena
     xs_rec = fa((size_t)Wcap * nh * XS_NSP * XREC); xs_cnt = ia((size_t)Wcap * nh);
     x2_d = fa((size_t)8 * n);
-    if (!S.seed || !S.cand_idx || !p1_cnt || !xs_cnt || !x2_d) return fail(-3, "activation arena overflow");
+    if (!S.seed || !S.cand_idx || !S.lp_cnt || !p1_cnt || !xs_cnt || !x2_d) return fail(-3, "activation arena overflow");
     S.nw = Wcap; S.G = 1; S.ctx = CTX; S.hctx = HCTX; S.maxc = 16;
     HIPCHK(hipMalloc(&d_gmax, 64));
     d_gmax_f = (float*)(d_gmax + 4);
