@@ -471,7 +471,8 @@ __global__ __launch_bounds__(512) void k_gemv_rows(GemmArgs a) {
 // logits[m][n] = sum_k X[m][k] E[n][k] for a decoder step's rows against the whole token
 // embedding (V = 51866 columns, 133 MB in fp16).  The rows are cut into a.row_groups groups
 // of RG = ceil(M / row_groups) <= 64 rows, each small enough to sit in LDS with all of K
-// (fp16, K 1280: <= 60 rows; 100 rows = 2 groups of 50); a workgroup stages its group's
+// (fp16, K 1280: <= 60 rows; the launcher uses it for <= 32 rows, one group — two groups
+// of 50 at 100 rows measured slower than k_vocab_2p's halves of K); a workgroup stages its group's
 // rows once, then every WAVE owns whole 16-column tiles (all of K: no cross-wave reduction,
 // no barrier in the loop), visiting tiles gw, gw + nwaves, ... so the weight stream is split
 // evenly over the group's waves.  Its weight fragments stream in chunks of VC k-steps, the
@@ -494,6 +495,27 @@ __global__ __launch_bounds__(512) void k_vocab_small(GemmArgs a) {
   const int m0 = grp * RG;
   const T* X = reinterpret_cast<const T*>(a.X);
   const T* W = reinterpret_cast<const T*>(a.W);
+  const int nt = (a.N + 15) / 16;
+  const int gw = cblk * 8 + wave, nw = ncblk * 8;
+  const int ntw = gw < nt ? (nt - 1 - gw) / nw + 1 : 0;  // tiles of this wave
+  const int J = ntw * nch;                                 // chunks of this wave
+  auto wsrc = [&](int j) {
+    const int t = gw + nw * (j / nch), s0 = (j % nch) * VC;
+    return W + (int64_t)min(t * 16 + r, a.N - 1) * K + s0 * 32 + 8 * g;
+  };
+  auto load_chunk = [&](int j, Frag<T>* wf) {
+    const T* wp = wsrc(j);
+    const int s0 = (j % nch) * VC;
+#pragma unroll
+    for (int c = 0; c < VC; ++c) frag_load_stream(wf[c], wp + (min(s0 + c, S - 1) - s0) * 32);
+  };
+  Frag<T> wa[VC], wb[VC];
+  float4_t acc[MT];
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt) acc[mt] = (float4_t){0.f, 0.f, 0.f, 0.f};
+  // the first weight chunk is issued before the X staging (it does not depend on X), so its
+  // HBM round trip overlaps the LayerNorm prologue's / the X rows' loads
+  if (J > 0) load_chunk(0, wa);
   if (a.xf32) {
     // the decoder's final LayerNorm (decoder.py:316) of the fp32 residual rows, recomputed
     // by every workgroup (<= 8 rows x K x 4 B from L2) instead of its own launch: one wave
@@ -553,25 +575,6 @@ __global__ __launch_bounds__(512) void k_vocab_small(GemmArgs a) {
     }
   }
   __syncthreads();
-  const int nt = (a.N + 15) / 16;
-  const int gw = cblk * 8 + wave, nw = ncblk * 8;
-  const int ntw = gw < nt ? (nt - 1 - gw) / nw + 1 : 0;  // tiles of this wave
-  const int J = ntw * nch;                                 // chunks of this wave
-  auto wsrc = [&](int j) {
-    const int t = gw + nw * (j / nch), s0 = (j % nch) * VC;
-    return W + (int64_t)min(t * 16 + r, a.N - 1) * K + s0 * 32 + 8 * g;
-  };
-  auto load_chunk = [&](int j, Frag<T>* wf) {
-    const T* wp = wsrc(j);
-    const int s0 = (j % nch) * VC;
-#pragma unroll
-    for (int c = 0; c < VC; ++c) frag_load_stream(wf[c], wp + (min(s0 + c, S - 1) - s0) * 32);
-  };
-  Frag<T> wa[VC], wb[VC];
-  float4_t acc[MT];
-#pragma unroll
-  for (int mt = 0; mt < MT; ++mt) acc[mt] = (float4_t){0.f, 0.f, 0.f, 0.f};
-  if (J > 0) load_chunk(0, wa);
   for (int j = 0; j < J; j += 2) {
     // chunk j in wa (chunk j+1 -> wb in flight), then chunk j+1 in wb (j+2 -> wa)
 #pragma unroll
@@ -614,6 +617,83 @@ __global__ __launch_bounds__(512) void k_vocab_small(GemmArgs a) {
           acc[mt] = (float4_t){0.f, 0.f, 0.f, 0.f};
         }
       }
+    }
+  }
+}
+
+// ============================================================ vocabulary projection, 33-112 rows
+// The decoder step's logits for a whole batch (20 windows x 5 beams = 100 rows) against
+// the token embedding (133 MB fp16): every row is resident in LDS, HALF of K at a time
+// (100 rows x 640 x 2 B = 128 KB), so X crosses L2 once per workgroup and pass (k_gemv_x
+// re-stages it per 256-deep subchunk with two barriers each, 85 us; row groups over all of
+// K stream every column twice, 89 us: profiles/r03/vocab_groups_ab.txt).  A workgroup of
+// 16 waves owns a contiguous range of <= 16 16-column tiles, one per wave; the wave keeps
+// its tile's MT accumulators across both passes and streams its weight rows in chunks of
+// VC k-steps, the next chunk in flight while one is multiplied.  Accumulation runs over the
+// k-steps in ascending order into one accumulator per 16 x 16 block, as in k_vocab_small and
+// k_gemv_x: a row's logits are bit-identical whichever kernel the batch size selects.
+template <int MT>
+__global__ __launch_bounds__(1024) void k_vocab_2p(GemmArgs a) {
+  constexpr int NW = 16, VC = 5;
+  extern __shared__ __attribute__((aligned(16))) char xs2[];
+  const int K = a.K, KH = K / 2, SH = KH / 32, nch = SH / VC;  // launcher: SH % VC == 0
+  const int xrow = KH * 2 + 16;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = lane & 15, g = lane >> 4;
+  const int nt = (a.N + 15) / 16;
+  const int t0 = (int)((int64_t)blockIdx.x * nt / gridDim.x), t1 = (int)((int64_t)(blockIdx.x + 1) * nt / gridDim.x);
+  const int tile = t0 + wave;
+  const bool act = tile < t1;
+  const half_t* X = reinterpret_cast<const half_t*>(a.X);
+  const half_t* wrow = reinterpret_cast<const half_t*>(a.W) + (int64_t)min(tile * 16 + r, a.N - 1) * K + 8 * g;
+  float4_t acc[MT];
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt) acc[mt] = (float4_t){0.f, 0.f, 0.f, 0.f};
+  Frag<half_t> wa[VC], wb[VC];
+  auto load_chunk = [&](int h, int c, Frag<half_t>* wf) {  // k-steps h*SH + c*VC .. +VC-1
+    const half_t* wp = wrow + (h * SH + c * VC) * 32;
+#pragma unroll
+    for (int u = 0; u < VC; ++u) frag_load_stream(wf[u], wp + u * 32);
+  };
+  const int cpr = KH * 2 / 16;  // 16 B chunks per staged row
+  for (int h = 0; h < 2; ++h) {
+    if (act) load_chunk(h, 0, wa);  // the pass's first weight chunk rides with the staging loads
+    if (h) __syncthreads();          // every wave is done with the first half's rows
+    for (int c = tid; c < a.M * cpr; c += 1024) {
+      const int row = c / cpr, col = c - row * cpr;
+      const int xr = a.x_rows ? a.x_rows[row] : row;
+      *reinterpret_cast<float4_t*>(xs2 + row * xrow + col * 16) =
+          *reinterpret_cast<const float4_t*>(reinterpret_cast<const char*>(X + (int64_t)xr * a.ldx + h * KH) + col * 16);
+    }
+    __syncthreads();
+    if (act) {
+      for (int c = 0; c < nch; ++c) {
+        Frag<half_t>* cur = (c & 1) ? wb : wa;
+        Frag<half_t>* nxt = (c & 1) ? wa : wb;
+        if (c + 1 < nch) load_chunk(h, c + 1, nxt);
+#pragma unroll
+        for (int u = 0; u < VC; ++u) {
+          const int ks = c * VC + u;
+#pragma unroll
+          for (int mt = 0; mt < MT; ++mt) {
+            Frag<half_t> xf;
+            frag_load(xf, reinterpret_cast<const half_t*>(xs2 + min(mt * 16 + r, a.M - 1) * xrow) + ks * 32 + 8 * g);
+            mfma_step(acc[mt], cur[u], xf);
+          }
+        }
+      }
+    }
+  }
+  if (!act) return;
+  // lane holds rows mt*16 + r, columns tile*16 + 4g .. +3
+  const int n = tile * 16 + 4 * g;
+  const auto rs = wt_rsrc(a.out_f32);
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt) {
+    const int m = mt * 16 + r;
+    if (m < a.M) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        if (n + e < a.N) wt_store1(rs, (m * a.ldo + n + e) * 4, acc[mt][e] + (a.bias ? a.bias[n + e] : 0.f));
     }
   }
 }
@@ -853,6 +933,28 @@ int launch_gemm_tiles(const GemmArgs& a, int epi, int tile_sel, hipStream_t st) 
         case 2: return go(std::integral_constant<int, 2>());
         case 3: return go(std::integral_constant<int, 3>());
         default: return go(std::integral_constant<int, 4>());
+      }
+    }
+    // k_vocab_2p: 33..112 fp16 rows resident in LDS, half of K per pass
+    if (sizeof(T) == 2 && vocab_small && epi == EPI_F32_COLS && a.N >= 16384 && a.M > 32 && a.M <= 112 && !a.xf32 &&
+        a.K % 320 == 0 && a.M * (a.K + 16) <= 150 * 1024) {
+      const int nt = (a.N + 15) / 16;
+      const int grid = std::max((nt + 15) / 16, std::min(256, nt));
+      const int lds = a.M * (a.K + 16);  // rows x (K / 2 halves x 2 B + 16)
+      auto go = [&](auto mtc) {
+        constexpr int MTV = decltype(mtc)::value;
+        static bool attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_vocab_2p<MTV>),
+                                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) == hipSuccess;
+        if (!attr) return -5;
+        k_vocab_2p<MTV><<<grid, 1024, lds, st>>>(a);
+        return 0;
+      };
+      switch ((a.M + 15) / 16) {
+        case 3: return go(std::integral_constant<int, 3>());
+        case 4: return go(std::integral_constant<int, 4>());
+        case 5: return go(std::integral_constant<int, 5>());
+        case 6: return go(std::integral_constant<int, 6>());
+        default: return go(std::integral_constant<int, 7>());
       }
     }
     if (mt >= 3 && epi == EPI_F32_COLS && a.N >= 16384) {

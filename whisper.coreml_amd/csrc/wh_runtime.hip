@@ -1620,7 +1620,9 @@ struct Ctx : public wh_ctx {
       if (cur_nwin < 1) return fail(-16, "no decode batch");
       const int per_step = 6 * Ld;
       proj_ev.resize(2 * per_step * iters);
-      for (auto& ev : proj_ev) HIPCHK(hipEventCreate(&ev));
+      // timing-only events: no system-scope fence (its L2 writeback / invalidate would be
+      // charged to the timed kernel; rocprofv3's kernel trace has none)
+      for (auto& ev : proj_ev) HIPCHK(hipEventCreateWithFlags(&ev, hipEventDisableSystemFence));
       double tot = 0;
       int launches = 0, rc = 0;
       // steps queued back to back as in decode_steps (no host sync between them)
