@@ -676,7 +676,16 @@ void launch_logit_rows(float* logits, int ldl, const DecState& s, const DecOpts&
   // k_logit_combine as its own launch)
   const char* fe = tune_env("WHISPER_HIP_LP_FUSED");
   const bool fused = !(fe && fe[0] == '0');
-  if (split && o.ts_begin > 0 && rows <= 32 && (o.ts_begin + 30) / 31 <= LP_THREADS * 4 && o.V - o.ts_begin <= LP_THREADS * 4) {
+  // tuning: WHISPER_HIP_LP_NS=16 / 32 forces the slice count past 32 rows (A/B)
+  const char* nse = tune_env("WHISPER_HIP_LP_NS");
+  const int ns_force = nse ? atoi(nse) : 0;
+  if (split && fused && ns_force == 16 && o.ts_begin > 0 && (o.ts_begin + 14) / 15 <= LP_THREADS * 8 &&
+      o.V - o.ts_begin <= LP_THREADS * 8) {
+    k_logit_part<16, 8, true><<<dim3(rows, 16), LP_THREADS, 0, st>>>(logits, ldl, s, o);
+    return;
+  }
+  if (split && o.ts_begin > 0 && (rows <= 32 || ns_force == 32) && (o.ts_begin + 30) / 31 <= LP_THREADS * 4 &&
+      o.V - o.ts_begin <= LP_THREADS * 4) {
     if (fused) {
       k_logit_part<32, 4, true><<<dim3(rows, 32), LP_THREADS, 0, st>>>(logits, ldl, s, o);
     } else {
