@@ -676,10 +676,12 @@ void launch_logit_rows(float* logits, int ldl, const DecState& s, const DecOpts&
   // k_logit_combine as its own launch)
   const char* fe = tune_env("WHISPER_HIP_LP_FUSED");
   const bool fused = !(fe && fe[0] == '0');
-  // tuning: WHISPER_HIP_LP_NS=16 / 32 forces the slice count past 32 rows (A/B)
+  // past 32 rows: 16 slices (15 text + timestamps, 8 elements per lane); 8 slices measured
+  // 3.5 us and 32 slices 10 us slower per 100-row step (profiles/r03/step_tail_ab.txt).
+  // Tuning: WHISPER_HIP_LP_NS=8 / 32 forces the other counts (A/B)
   const char* nse = tune_env("WHISPER_HIP_LP_NS");
-  const int ns_force = nse ? atoi(nse) : 0;
-  if (split && fused && ns_force == 16 && o.ts_begin > 0 && (o.ts_begin + 14) / 15 <= LP_THREADS * 8 &&
+  const int ns_force = nse ? atoi(nse) : 16;  // slices past 32 rows
+  if (split && fused && rows > 32 && ns_force == 16 && o.ts_begin > 0 && (o.ts_begin + 14) / 15 <= LP_THREADS * 8 &&
       o.V - o.ts_begin <= LP_THREADS * 8) {
     k_logit_part<16, 8, true><<<dim3(rows, 16), LP_THREADS, 0, st>>>(logits, ldl, s, o);
     return;

@@ -632,12 +632,12 @@ __global__ __launch_bounds__(512) void k_vocab_small(GemmArgs a) {
 // VC k-steps, the next chunk in flight while one is multiplied.  Accumulation runs over the
 // k-steps in ascending order into one accumulator per 16 x 16 block, as in k_vocab_small and
 // k_gemv_x: a row's logits are bit-identical whichever kernel the batch size selects.
-template <int MT>
+template <int MT, int DEPTH>
 __global__ __launch_bounds__(1024) void k_vocab_2p(GemmArgs a) {
-  constexpr int NW = 16, VC = 5;
+  constexpr int NW = 16, VC = DEPTH > 2 ? 4 : 5, KH = 640, SH = KH / 32, NCH = SH / VC;  // K 1280 (launcher)
+  constexpr int XROW = KH * 2 + 16;
   extern __shared__ __attribute__((aligned(16))) char xs2[];
-  const int K = a.K, KH = K / 2, SH = KH / 32, nch = SH / VC;  // launcher: SH % VC == 0
-  const int xrow = KH * 2 + 16;
+  constexpr int K = 2 * KH;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = lane & 15, g = lane >> 4;
   const int nt = (a.N + 15) / 16;
   const int t0 = (int)((int64_t)blockIdx.x * nt / gridDim.x), t1 = (int)((int64_t)(blockIdx.x + 1) * nt / gridDim.x);
@@ -648,36 +648,41 @@ __global__ __launch_bounds__(1024) void k_vocab_2p(GemmArgs a) {
   float4_t acc[MT];
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt) acc[mt] = (float4_t){0.f, 0.f, 0.f, 0.f};
-  Frag<half_t> wa[VC], wb[VC];
-  auto load_chunk = [&](int h, int c, Frag<half_t>* wf) {  // k-steps h*SH + c*VC .. +VC-1
+  // DEPTH weight chunks of VC k-steps: DEPTH - 1 in flight while one is multiplied
+  Frag<half_t> wbuf[DEPTH][VC];
+  auto load_chunk = [&](int h, int c, Frag<half_t>(&wf)[VC]) {  // k-steps h*SH + c*VC .. +VC-1
     const half_t* wp = wrow + (h * SH + c * VC) * 32;
 #pragma unroll
     for (int u = 0; u < VC; ++u) frag_load_stream(wf[u], wp + u * 32);
   };
-  const int cpr = KH * 2 / 16;  // 16 B chunks per staged row
+  constexpr int CPR = KH * 2 / 16;  // 16 B chunks per staged row
+#pragma unroll
   for (int h = 0; h < 2; ++h) {
-    if (act) load_chunk(h, 0, wa);  // the pass's first weight chunk rides with the staging loads
-    if (h) __syncthreads();          // every wave is done with the first half's rows
-    for (int c = tid; c < a.M * cpr; c += 1024) {
-      const int row = c / cpr, col = c - row * cpr;
+    // the pass's first DEPTH - 1 weight chunks ride with the staging loads
+    if (act) {
+#pragma unroll
+      for (int c = 0; c < DEPTH - 1 && c < NCH; ++c) load_chunk(h, c, wbuf[c]);
+    }
+    if (h) __syncthreads();  // every wave is done with the first half's rows
+    for (int c = tid; c < a.M * CPR; c += 1024) {
+      const int row = c / CPR, col = c - row * CPR;
       const int xr = a.x_rows ? a.x_rows[row] : row;
-      *reinterpret_cast<float4_t*>(xs2 + row * xrow + col * 16) =
+      *reinterpret_cast<float4_t*>(xs2 + row * XROW + col * 16) =
           *reinterpret_cast<const float4_t*>(reinterpret_cast<const char*>(X + (int64_t)xr * a.ldx + h * KH) + col * 16);
     }
     __syncthreads();
     if (act) {
-      for (int c = 0; c < nch; ++c) {
-        Frag<half_t>* cur = (c & 1) ? wb : wa;
-        Frag<half_t>* nxt = (c & 1) ? wa : wb;
-        if (c + 1 < nch) load_chunk(h, c + 1, nxt);
+#pragma unroll
+      for (int c = 0; c < NCH; ++c) {
+        if (c + DEPTH - 1 < NCH) load_chunk(h, c + DEPTH - 1, wbuf[(c + DEPTH - 1) % DEPTH]);
 #pragma unroll
         for (int u = 0; u < VC; ++u) {
           const int ks = c * VC + u;
 #pragma unroll
           for (int mt = 0; mt < MT; ++mt) {
             Frag<half_t> xf;
-            frag_load(xf, reinterpret_cast<const half_t*>(xs2 + min(mt * 16 + r, a.M - 1) * xrow) + ks * 32 + 8 * g);
-            mfma_step(acc[mt], cur[u], xf);
+            frag_load(xf, reinterpret_cast<const half_t*>(xs2 + min(mt * 16 + r, a.M - 1) * XROW) + ks * 32 + 8 * g);
+            mfma_step(acc[mt], wbuf[c % DEPTH][u], xf);
           }
         }
       }
@@ -937,16 +942,24 @@ int launch_gemm_tiles(const GemmArgs& a, int epi, int tile_sel, hipStream_t st) 
     }
     // k_vocab_2p: 33..112 fp16 rows resident in LDS, half of K per pass
     if (sizeof(T) == 2 && vocab_small && epi == EPI_F32_COLS && a.N >= 16384 && a.M > 32 && a.M <= 112 && !a.xf32 &&
-        a.K % 320 == 0 && a.M * (a.K + 16) <= 150 * 1024) {
+        a.K == 1280 && a.M * (a.K + 16) <= 150 * 1024) {
+      // two 4-step weight chunks in flight per wave (DEPTH 3; WHISPER_HIP_V2P_DEPTH=2 in the
+      // tuning build: one 5-step chunk) — step graph 3.5456 -> 3.5413 ms at 20 windows,
+      // profiles/r03/step_tail_ab.txt
+      const char* de = tune_env("WHISPER_HIP_V2P_DEPTH");
+      const bool d3 = !(de && de[0] == '2');
       const int nt = (a.N + 15) / 16;
       const int grid = std::max((nt + 15) / 16, std::min(256, nt));
       const int lds = a.M * (a.K + 16);  // rows x (K / 2 halves x 2 B + 16)
       auto go = [&](auto mtc) {
         constexpr int MTV = decltype(mtc)::value;
-        static bool attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_vocab_2p<MTV>),
+        static bool attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_vocab_2p<MTV, 2>),
+                                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) == hipSuccess &&
+                           hipFuncSetAttribute(reinterpret_cast<const void*>(&k_vocab_2p<MTV, 3>),
                                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) == hipSuccess;
         if (!attr) return -5;
-        k_vocab_2p<MTV><<<grid, 1024, lds, st>>>(a);
+        if (d3) k_vocab_2p<MTV, 3><<<grid, 1024, lds, st>>>(a);
+        else k_vocab_2p<MTV, 2><<<grid, 1024, lds, st>>>(a);
         return 0;
       };
       switch ((a.M + 15) / 16) {
