@@ -283,10 +283,11 @@ def main():
     task = DecodingTask(model, whisper.DecodingOptions(language="en", beam_size=args.beam))
     model.ctx.decode_begin(task.wh_opts(), [task.initial_tokens] * n_win, [task.sot_index] * n_win)
     rows = n_win * args.beam
-    # in-step: every k_proj of 3 eager steps bracketed by HIP events on the context
+    # in-step: every k_proj of 6 eager steps bracketed by HIP events on the context
     # stream, each behind its real producer kernel (what rocprof sees in the step);
     # back-to-back: the same launches queued without their producers (time_stage 2)
-    gemv_ms = model.ctx.time_stage(7, 3)
+    model.ctx.time_stage(7, 2)  # warm-up (without it the same tree read 7.0-8.1 us run to run)
+    gemv_ms = model.ctx.time_stage(7, 6)
     gemv_b2b_ms = model.ctx.time_stage(2, 3)
     kern = model.ctx.step_kernels(n_win, args.beam)  # what the library runs for this batch
     p1 = kern["proj"] == "k_proj1"
