@@ -995,7 +995,12 @@ int launch_gemm_tiles(const GemmArgs& a, int epi, int tile_sel, hipStream_t st) 
 #undef LAUNCHV
       return 0;
     }
-    if (mt >= 3 && (epi == EPI_PARTIAL || (a.N + 63) / 64 >= 70)) {  // tall-skinny: X shared via LDS by 4 column tiles
+    // tall-skinny split-K partials: X shared via LDS by 4 column tiles.  Every other
+    // epilogue at <= 128 rows runs k_gemv_rows below whatever the row count, so a row's
+    // summation order (8 waves' k-step shares, summed in fixed order) does not depend on
+    // how many rows share the launch — the first pass of a batch of windows is
+    // batch-invariant like the step (fc1 used to switch to k_gemv_x from 33 rows)
+    if (mt >= 3 && epi == EPI_PARTIAL) {
       dim3 gx((a.N + 63) / 64, (a.M + 16 * rows_per - 1) / (16 * rows_per), ks);
 #define LAUNCHX(MT_)                                                                            \
   switch (epi) {                                                                               \

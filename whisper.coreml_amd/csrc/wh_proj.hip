@@ -85,7 +85,10 @@ int launch_proj_partial(const GemmArgs& a, int max_z, hipStream_t st, int* z_out
     const Cfg& k = CFGS[c];
     if (S % (k.kw * k.nstep)) continue;
     const int z = S / (k.kw * k.nstep);
-    if (z > 16 || tab.e[mt - 1][c].lds > LDS_MAX) continue;
+    // feasibility at the largest row tile count (MT 7): a configuration whose LDS fits
+    // only at fewer rows would give small batches another K split (and so other slab
+    // sums) than large ones — caught by test_gpu_batch.py::test_batch_invariance_fp16
+    if (z > 16 || tab.e[6][c].lds > LDS_MAX) continue;
     const int wgs = (a.N + 16 * k.nsub - 1) / (16 * k.nsub) * z;
     if (forced >= 0) {
       if (c == forced) best = c, best_wgs = wgs, best_z = z;
