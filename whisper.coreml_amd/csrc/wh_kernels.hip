@@ -359,6 +359,81 @@ __global__ __launch_bounds__(64) void k_self_attn(const T* __restrict__ q, int l
   const int64_t head_stride = (int64_t)ctx * 64;
   const int64_t wbase = (int64_t)w * nbeam;
   auto kv_off = [&](int slot, int p) -> int64_t { return ((wbase + slot) * H + h) * head_stride + (int64_t)p * 64; };
+  if constexpr (sizeof(T) == 2) {
+    // round 3 (fp16): the k_self_attn_qkv schedule — the ancestry of every context
+    // position in the first round trip (8 per lane, with q), then per 128-key pass K
+    // (lane per key) and V (8 lanes per key) in ONE round trip with an online softmax
+    // across passes; the round-2 form (ancestry, then K, then V four keys per lane at a
+    // time) took up to 8 dependent round trips at mid context (9.6 us average per layer
+    // over a one-window decode, profiles/r03/bench_eager_rocprof_summary.txt)
+    int sv[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) sv[i] = an[min(lane + 64 * i, ctx - 1)];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int pp = lane + 64 * i;
+      if (pp <= pos) slot_of[pp] = pp == pos ? sl : sv[i];
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // one wave: its own LDS writes
+    const int kg = lane >> 3, dc = (lane & 7) * 8;
+    float m = -INFINITY, lsum = 0.f, o[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] = 0.f;
+    for (int p0 = 0; p0 <= pos; p0 += 128) {
+      const int pa = min(p0 + lane, pos), pb = min(p0 + 64 + lane, pos);
+      const T* ra = kc + kv_off(slot_of[pa], pa);
+      const T* rb = kc + kv_off(slot_of[pb], pb);
+      Frag<T> ka[8], kb[8], vf[16];
+#pragma unroll
+      for (int c = 0; c < 8; ++c) frag_load(ka[c], ra + 8 * c);
+#pragma unroll
+      for (int c = 0; c < 8; ++c) frag_load(kb[c], rb + 8 * c);
+#pragma unroll
+      for (int u = 0; u < 16; ++u) {
+        const int pc = min(p0 + kg + 8 * u, pos);
+        frag_load(vf[u], vc + kv_off(slot_of[pc], pc) + dc);
+      }
+      __builtin_amdgcn_sched_barrier(0);  // every load of the pass ahead of the math
+      float sa = 0.f, sb = 0.f;
+#pragma unroll
+      for (int c = 0; c < 8; ++c)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          sa += qv[8 * c + e] * to_f32(ka[c].v[e]);
+          sb += qv[8 * c + e] * to_f32(kb[c].v[e]);
+        }
+      const bool va = p0 + lane <= pos, vb = p0 + 64 + lane <= pos;
+      const float mp = wave_max(fmaxf(va ? sa : -INFINITY, vb ? sb : -INFINITY));
+      const float mn = fmaxf(m, mp), scale = __expf(m - mn);
+      m = mn;
+      const float ea = va ? __expf(sa - m) : 0.f, eb = vb ? __expf(sb - m) : 0.f;
+      lsum = lsum * scale + wave_sum(ea + eb);
+      sc[lane] = ea;
+      sc[64 + lane] = eb;
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o[e] *= scale;
+#pragma unroll
+      for (int u = 0; u < 16; ++u) {
+        const float pw = sc[kg + 8 * u];  // 0 past the end
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o[e] += pw * to_f32(vf[u].v[e]);
+      }
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      o[e] += __shfl_xor(o[e], 8, 64);
+      o[e] += __shfl_xor(o[e], 16, 64);
+      o[e] += __shfl_xor(o[e], 32, 64);
+    }
+    if (kg == 0) {
+      const float inv = 1.f / lsum;
+      T* op = out + (int64_t)row * ldo + h * 64 + dc;
+      store4(op, o[0] * inv, o[1] * inv, o[2] * inv, o[3] * inv);
+      store4(op + 4, o[4] * inv, o[5] * inv, o[6] * inv, o[7] * inv);
+    }
+    return;
+  }
   // scores: lane per key
   float mx = -INFINITY;
   for (int p = lane; p <= pos; p += 64) {
@@ -1155,7 +1230,9 @@ int xattn_seg_grid(int npair, int nsp, int smax) {
     if (nwg >= 192 && ppw * nsp <= smax) return nwg;
   }
   if (k > smax / 8) k = smax / 8;
-  int nwg = k == 1 ? (nseg < 256 ? nseg : 256) : (nseg + 8 * k - 1) / (8 * k);
+  // k = 1: spread over 200 workgroups, not 256 (1 / 2 / 4 windows 10.2 -> 9.6, 11.2 -> 11.1,
+  // 14.1 -> 13.9 us, profiles/r03/xattn_grid_few_windows.txt)
+  int nwg = k == 1 ? (nseg < 200 ? nseg : 200) : (nseg + 8 * k - 1) / (8 * k);
   if ((nseg + nwg - 1) / nwg > smax) nwg = (nseg + smax - 1) / smax;
   return nwg;
 }
