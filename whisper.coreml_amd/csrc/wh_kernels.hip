@@ -65,20 +65,20 @@ void launch_layernorm(const float* x, T* y, const float* g, const float* b, int 
 // x[r] += bias + sum_s part[s][r] (fixed order: deterministic split-K reduction of the
 // residual GEMVs), then y = LayerNorm(x).  One 256-thread block per row; every load
 // of the row is issued before the first reduction (latency-bound at decode sizes).
-template <typename T, int NS>
-__global__ __launch_bounds__(256) void k_resid_ln(float* __restrict__ x, const float* __restrict__ part, int nsplit,
+template <typename T, int NS, int MAXV = 2>
+__global__ __launch_bounds__(512) void k_resid_ln(float* __restrict__ x, const float* __restrict__ part, int nsplit,
                                                   int64_t part_stride, const float* __restrict__ bias,
                                                   T* __restrict__ y, const float* __restrict__ gamma,
                                                   const float* __restrict__ beta, int n, float eps) {
-  __shared__ float red[2][4];
-  const int row = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  __shared__ float red[2][8];
+  const int row = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, NT = blockDim.x, nwv = NT >> 6;
   float* xr = x + (int64_t)row * n;
-  constexpr int MAXV = 2;  // n <= 256 * 4 * 2 = 2048
+  // NT * 4 * MAXV >= n (n <= 2048): 256 threads x 2 float4, or ceil(n / 256) waves x 1
   const int nv = n >> 2;
   float4_t v[MAXV], gm[MAXV], bt[MAXV];
 #pragma unroll
   for (int i = 0; i < MAXV; ++i) {
-    const int c = tid + 256 * i;
+    const int c = tid + NT * i;
     if (c < nv) {
       // LayerNorm's gamma / beta ride with the first round trip, not after the reductions
       gm[i] = load4f(gamma + 4 * c);
@@ -98,18 +98,20 @@ __global__ __launch_bounds__(256) void k_resid_ln(float* __restrict__ x, const f
   float s = 0.f;
 #pragma unroll
   for (int i = 0; i < MAXV; ++i)
-    if (tid + 256 * i < nv) {
-      store4(xr + 4 * (tid + 256 * i), v[i][0], v[i][1], v[i][2], v[i][3]);
+    if (tid + NT * i < nv) {
+      store4(xr + 4 * (tid + NT * i), v[i][0], v[i][1], v[i][2], v[i][3]);
       s += v[i][0] + v[i][1] + v[i][2] + v[i][3];
     }
   s = wave_sum(s);
   if (lane == 0) red[0][wv] = s;
   __syncthreads();
-  const float mean = (red[0][0] + red[0][1] + red[0][2] + red[0][3]) / (float)n;
+  float tot = 0.f;
+  for (int k = 0; k < nwv; ++k) tot += red[0][k];
+  const float mean = tot / (float)n;
   float q = 0.f;
 #pragma unroll
   for (int i = 0; i < MAXV; ++i)
-    if (tid + 256 * i < nv) {
+    if (tid + NT * i < nv) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const float d = v[i][j] - mean;
@@ -119,11 +121,13 @@ __global__ __launch_bounds__(256) void k_resid_ln(float* __restrict__ x, const f
   q = wave_sum(q);
   if (lane == 0) red[1][wv] = q;
   __syncthreads();
-  const float rstd = rsqrtf((red[1][0] + red[1][1] + red[1][2] + red[1][3]) / (float)n + eps);
+  float qt = 0.f;
+  for (int k = 0; k < nwv; ++k) qt += red[1][k];
+  const float rstd = rsqrtf(qt / (float)n + eps);
   T* yr = y + (int64_t)row * n;
 #pragma unroll
   for (int i = 0; i < MAXV; ++i) {
-    const int c = tid + 256 * i;
+    const int c = tid + NT * i;
     if (c < nv)
       store4(yr + 4 * c, (v[i][0] - mean) * rstd * gm[i][0] + bt[i][0], (v[i][1] - mean) * rstd * gm[i][1] + bt[i][1],
              (v[i][2] - mean) * rstd * gm[i][2] + bt[i][2], (v[i][3] - mean) * rstd * gm[i][3] + bt[i][3]);
@@ -134,12 +138,20 @@ template <typename T>
 void launch_resid_ln(float* x, const float* part, int nsplit, int64_t part_stride, const float* bias, T* y,
                      const float* g, const float* b, int rows, int n, float eps, hipStream_t st) {
   if (rows <= 0) return;
-  if (nsplit <= 0)
-    k_resid_ln<T, 0><<<rows, 256, 0, st>>>(x, part, 0, part_stride, bias, y, g, b, n, eps);
-  else if (nsplit <= 4)
-    k_resid_ln<T, 4><<<rows, 256, 0, st>>>(x, part, nsplit, part_stride, bias, y, g, b, n, eps);
-  else
-    k_resid_ln<T, 16><<<rows, 256, 0, st>>>(x, part, nsplit, part_stride, bias, y, g, b, n, eps);
+  // one float4 per thread (n <= 2048; 1280: 5 waves); tuning builds WHISPER_HIP_RLN_256=1
+  // for the round-3 form (256 threads, up to two float4 each)
+  const char* e = tune_env("WHISPER_HIP_RLN_256");
+  const int nt = (e && atoi(e) == 1) ? 256 : ((n >> 2) + 63) / 64 * 64;
+#define RLN(NS_, MV_) \
+  k_resid_ln<T, NS_, MV_><<<rows, nt, 0, st>>>(x, part, NS_ ? nsplit : 0, part_stride, bias, y, g, b, n, eps)
+  if (nsplit <= 0) {
+    if (nt == 256) RLN(0, 2); else RLN(0, 1);
+  } else if (nsplit <= 4) {
+    if (nt == 256) RLN(4, 2); else RLN(4, 1);
+  } else {
+    if (nt == 256) RLN(16, 2); else RLN(16, 1);
+  }
+#undef RLN
 }
 
 // ============================================================ encoder flash attention (non-causal)
