@@ -16,11 +16,19 @@ reports whether the merged segments equal it (``verify``).
 
 value = (audio seconds of the whole file x steps) / (max over ranks of the timed
 wall time) = whole-job xRT.  rank 0 prints one JSON line.
+
+Launch: under torch.distributed.run (WORLD_SIZE set) every process is one rank.
+Without it, ``--gpus N`` > 1 starts the N ranks itself (``launch_ranks``): N child
+processes of this script with RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set,
+spawned before this process touches the GPU; the parent waits for all of them and
+exits non-zero if any rank fails.  Every rank checks world == --gpus.
 """
 
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -57,21 +65,69 @@ def parse():
     p.add_argument("--dump", default="", help="write the last step's segments (tokens, avg_logprob) as JSON")
     p.add_argument("--word-timestamps", type=int, default=0,
                    help="config 5: transcribe(word_timestamps=True) (alignment + DTW on the GPU per window)")
+    p.add_argument("--backend", default="nccl", help="torch.distributed backend of the ranks (nccl = RCCL)")
+    p.add_argument("--launch-check", type=int, default=0,
+                   help="only bring the ranks up, all-gather (rank, world) and print it from rank 0 (no GPU work)")
     return p.parse_args()
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(args):
+    """--gpus N without an external launcher: run this script as N rank processes.
+
+    Called before anything in this process imports torch.cuda or the HIP library
+    (no exec: the children are new processes, this one only waits).  Returns the
+    exit code: 0 when every rank exited 0, else the first non-zero code."""
+    port = _free_port()
+    procs = []
+    for r in range(args.gpus):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(args.gpus), LOCAL_WORLD_SIZE=str(args.gpus),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    codes = [p.wait() for p in procs]
+    bad = [(r, c) for r, c in enumerate(codes) if c != 0]
+    if bad:
+        print(f"bench.py: rank(s) failed: {bad}", file=sys.stderr, flush=True)
+        return bad[0][1] if bad[0][1] > 0 else 1
+    return 0
 
 
 def dist_setup(args):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE {world}")
     pg = None
     if world > 1:
-        import torch
         import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl")
+        if args.backend == "nccl":
+            import torch
+            torch.cuda.set_device(local)
+        dist.init_process_group(args.backend)
+        assert dist.get_world_size() == args.gpus
         pg = dist
     return world, rank, local, pg
+
+
+def launch_check(args):
+    """--launch-check 1: the ranks came up; rank 0 prints every rank's (rank, world)."""
+    world, rank, _, pg = dist_setup(args)
+    seen = [(rank, world)]
+    if pg is not None:
+        seen = [None] * world
+        pg.all_gather_object(seen, (rank, pg.get_world_size()))
+    if rank == 0:
+        print(json.dumps({"launch_check": True, "n_gpus": world, "ranks": seen}), flush=True)
+    if pg is not None:
+        pg.destroy_process_group()
 
 
 def allreduce_max(pg, x: float) -> float:
@@ -145,6 +201,48 @@ def encoder_flops(dims):
     return conv + L * block
 
 
+def cpu_topology():
+    """Threads for the CPU baseline (the physical cores of one socket).
+
+    The physical cores of the socket holding most of this process's allowed CPUs
+    (os.sched_getaffinity + sysfs topology), capped by the CPU share the process is
+    given: the cgroup cpu.max quota, else OMP_NUM_THREADS when the environment sets it
+    (the GPU pool gives each one-GPU job a 16-CPU share and exports 16)."""
+    allowed = sorted(os.sched_getaffinity(0))
+    sockets = {}
+    for c in allowed:
+        base = f"/sys/devices/system/cpu/cpu{c}/topology/"
+        try:
+            with open(base + "physical_package_id") as f:
+                pkg = int(f.read())
+            with open(base + "core_id") as f:
+                core = int(f.read())
+        except (OSError, ValueError):
+            pkg, core = 0, c
+        sockets.setdefault(pkg, set()).add(core)
+    socket_cores = max((len(v) for v in sockets.values()), default=len(allowed))
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, period = f.read().split()[:2]
+        if q != "max":
+            quota = max(1, int(int(q) / int(period)))
+    except (OSError, ValueError):
+        pass
+    omp = os.environ.get("OMP_NUM_THREADS")
+    omp = int(omp) if omp and omp.isdigit() else None
+    share, why = None, "one socket's physical cores"
+    if quota is not None:
+        share, why = quota, f"capped by the cgroup CPU quota ({quota} CPUs)"
+    elif omp is not None:
+        share, why = omp, f"capped by the job's CPU share (OMP_NUM_THREADS={omp})"
+    threads = min(socket_cores, share) if share else socket_cores
+    if share and share >= socket_cores:
+        why = "one socket's physical cores"
+    return dict(threads=threads, socket_physical_cores=socket_cores, sockets=len(sockets), allowed_cpus=len(allowed),
+                cgroup_cpus=quota, omp_num_threads=omp, why=why)
+
+
 def cpu_baseline(model_name, sd, audio, beams, n_steps):
     """The oracle (CPU fp32 restatement, oracle/ref_whisper.py) decoding one 30 s window
     exactly as the reference's DecodingTask does (encoder, first pass, then every
@@ -154,6 +252,8 @@ def cpu_baseline(model_name, sd, audio, beams, n_steps):
     import torch
     from oracle import ref_whisper as R
     from whisper import synthetic as S
+    topo = cpu_topology()
+    torch.set_num_threads(topo["threads"])
     threads = torch.get_num_threads()
     cpu_model = "unknown"
     try:
@@ -176,7 +276,7 @@ def cpu_baseline(model_name, sd, audio, beams, n_steps):
     per_window = t_enc + t_dec * (224 / steps)
     kind = "the whole window" if not n_steps else f"{steps} steps scaled to 224"
     return dict(value=round(30.0 / per_window, 4), unit="xRT (audio-s/s)", cores=threads, cpu_model=cpu_model,
-                kind="port",
+                kind="port", topology=topo,
                 sample=f"1 window (30 s) of {model_name}, beam {beams}, {kind}: encoder {t_enc:.1f} s + decode "
                        f"{t_dec:.1f} s ({len(res.tokens)} tokens; oracle/ref_whisper.py decode with the reference's "
                        f"beam search, torch CPU fp32, {threads} threads of {cpu_model})")
@@ -184,6 +284,10 @@ def cpu_baseline(model_name, sd, audio, beams, n_steps):
 
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args))
+    if args.launch_check:
+        return launch_check(args)
     world, rank, local, pg = dist_setup(args)
     import whisper
     from whisper import distributed as D
@@ -329,7 +433,7 @@ def main():
         "metric": "xRT (audio-s/s) large-v3 beam=5 @1/2/4/8 GPU; p50 per-token decode ms",
         "value": round(file_seconds * args.steps / elapsed_max, 3),
         "unit": "audio-s/s",
-        "n_gpus": world,
+        "n_gpus": pg.get_world_size() if pg is not None else world,
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": round(elapsed_max * 1e3 / args.steps, 2),
@@ -357,7 +461,10 @@ def main():
                      "frac": round(gbs(gemv_bytes, gemv_ms) / HBM_PEAK_GBS, 4),
                      "traffic": traffic, "bytes_per_launch": gemv_bytes, "ms_per_launch": round(gemv_ms, 5),
                      "timing": "HIP events around each launch inside eager decoder steps",
-                     "ms_per_launch_back_to_back": round(gemv_b2b_ms, 5)},
+                     "ms_per_launch_back_to_back": round(gemv_b2b_ms, 5),
+                     "back_to_back_note": "time_stage 2: the six projections of each layer queued without their "
+                                          "producers; on the k_proj1 path the non-deferred fc2 and the plain QKV "
+                                          "LayerNorm prologue (the step itself defers fc2's residual)"},
         "roofline_overall": overall,
         "roofline_cross_attn": {"bound": "hbm", "kernel": f"{kern['xattn']} ({n_win} windows x {args.beam} beams)",
                                 "achieved": round(gbs(xattn_bytes, xattn_ms), 1), "peak": HBM_PEAK_GBS,

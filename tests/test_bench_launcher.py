@@ -1,0 +1,53 @@
+"""bench.py's own rank launcher (CPU, gloo): ``--gpus N`` without torch.distributed.run
+starts N rank processes, each sees WORLD_SIZE == N, rank 0 prints the line, and a
+failing rank makes the launcher exit non-zero.  No GPU is touched (--launch-check)."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+BENCH = os.path.join(REPO, "bench.py")
+
+
+def _run(args, env_extra=None, timeout=180):
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR",
+                                                             "MASTER_PORT")}
+    env.update(env_extra or {})
+    return subprocess.run([sys.executable, BENCH] + args, capture_output=True, text=True, timeout=timeout, env=env)
+
+
+def _json_lines(out):
+    return [json.loads(line) for line in out.splitlines() if line.startswith("{")]
+
+
+@pytest.mark.parametrize("n", [2, 3])
+def test_launcher_brings_up_n_ranks(n):
+    p = _run(["--gpus", str(n), "--launch-check", "1", "--backend", "gloo"])
+    assert p.returncode == 0, p.stderr
+    lines = _json_lines(p.stdout)
+    assert len(lines) == 1, p.stdout  # rank 0 only
+    assert lines[0]["n_gpus"] == n
+    assert sorted(map(tuple, lines[0]["ranks"])) == [(r, n) for r in range(n)]
+
+
+def test_launcher_single_gpu_runs_in_process():
+    p = _run(["--gpus", "1", "--launch-check", "1", "--backend", "gloo"])
+    assert p.returncode == 0, p.stderr
+    assert _json_lines(p.stdout) == [{"launch_check": True, "n_gpus": 1, "ranks": [[0, 1]]}]
+
+
+def test_launcher_fails_when_a_rank_fails():
+    p = _run(["--gpus", "2", "--launch-check", "1", "--backend", "no-such-backend"])
+    assert p.returncode != 0
+    assert "rank(s) failed" in p.stderr
+
+
+def test_world_must_match_gpus():
+    # an external launcher's world size that disagrees with --gpus is refused
+    p = _run(["--gpus", "1", "--launch-check", "1", "--backend", "gloo"],
+             env_extra=dict(WORLD_SIZE="2", RANK="0", LOCAL_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT="29999"))
+    assert p.returncode != 0
+    assert "WORLD_SIZE 2" in p.stderr

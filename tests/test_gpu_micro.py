@@ -111,6 +111,7 @@ def test_decode_tokens(micro, window_mel, key, opts):
         assert agree >= min(need, n)
 
 
+@pytest.mark.parametrize("micro", ["fp32"], indirect=True)  # segment-exact parity is an fp32 claim
 @pytest.mark.parametrize("run,schedule", [("clip_beam", "auto"), ("clip_greedy", "auto"), ("seq_greedy", "auto"), ("seq_beam", "auto"),
                                           ("clip_beam", "sequential"), ("clip_greedy", "sequential")])
 def test_transcribe_segments(micro, run, schedule):
@@ -118,9 +119,7 @@ def test_transcribe_segments(micro, run, schedule):
     the encoder and step graph together); "sequential" is the reference's loop."""
     import whisper
     from whisper import synthetic as S
-    m, dt = micro
-    if dt != "fp32":
-        pytest.skip("segment-exact parity is an fp32 claim")
+    m, _ = micro
     with open(os.path.join(GOLDEN, "micro_transcribe.json")) as f:
         gt = json.load(f)
     kw = dict(gt["runs"][run])
@@ -133,6 +132,7 @@ def test_transcribe_segments(micro, run, schedule):
         assert a["start"] == pytest.approx(b["start"]) and a["end"] == pytest.approx(b["end"])
 
 
+@pytest.mark.parametrize("micro", ["fp32"], indirect=True)  # segment-exact parity is an fp32 claim
 @pytest.mark.parametrize("run", ["clip_greedy", "clip_beam"])
 @pytest.mark.parametrize("world", [2, 3])
 def test_sharded_replay_equals_reference(micro, run, world):
@@ -141,9 +141,7 @@ def test_sharded_replay_equals_reference(micro, run, world):
     segments must equal the reference transcribe() of the whole file."""
     from whisper import distributed as D
     from whisper import synthetic as S
-    m, dt = micro
-    if dt != "fp32":
-        pytest.skip("segment-exact parity is an fp32 claim")
+    m, _ = micro
     with open(os.path.join(GOLDEN, "micro_transcribe.json")) as f:
         gt = json.load(f)
     kw = dict(gt["runs"][run])

@@ -676,21 +676,23 @@ void launch_logit_rows(float* logits, int ldl, const DecState& s, const DecOpts&
   // k_logit_combine as its own launch)
   const char* fe = tune_env("WHISPER_HIP_LP_FUSED");
   const bool fused = !(fe && fe[0] == '0');
-  // Every batch of >= 2 windows (> 8 rows) selects with 16 slices (15 text + timestamps,
-  // 8 elements per lane): the per-slice normaliser sums, hence a row's log-probabilities to
-  // the last bit, then do not depend on the batch size (batch invariance);
-  // at 100 rows 8 slices measured 3.5 us and 32 slices 10 us slower per step
-  // (profiles/r03/step_tail_ab.txt).  One window keeps 32 slices (its latency path).
+  // Every batch of >= 2 windows selects with 16 slices (15 text + timestamps, 8 elements
+  // per lane): the per-slice normaliser sums, hence a row's log-probabilities to the last
+  // bit, then do not depend on the batch size (batch invariance); at 100
+  // rows 8 slices measured 3.5 us and 32 slices 10 us slower per step
+  // (profiles/r03/step_tail_ab.txt).  One window keeps 32 slices (its latency path) —
+  // the same window-count cut as the k_proj1 layers (wh_runtime.hip p1_active), so the
+  // rule holds for greedy and small beams too.
   // Tuning: WHISPER_HIP_LP_NS=8 / 32 forces the other counts (A/B)
   const char* nse = tune_env("WHISPER_HIP_LP_NS");
-  const int ns_force = nse ? atoi(nse) : 16;  // slices past 8 rows
-  constexpr int ONE_WIN = 8;  // the rows the k_proj1 path serves (wh_proj.h P1_RMAX): same cut
-  if (split && fused && rows > ONE_WIN && ns_force == 16 && o.ts_begin > 0 &&
+  const int ns_force = nse ? atoi(nse) : 16;  // slices for >= 2 windows
+  const bool one_win = nwin == 1;
+  if (split && fused && !one_win && ns_force == 16 && o.ts_begin > 0 &&
       (o.ts_begin + 14) / 15 <= LP_THREADS * 8 && o.V - o.ts_begin <= LP_THREADS * 8) {
     k_logit_part<16, 8, true><<<dim3(rows, 16), LP_THREADS, 0, st>>>(logits, ldl, s, o);
     return;
   }
-  if (split && o.ts_begin > 0 && (rows <= ONE_WIN || ns_force == 32) && (o.ts_begin + 30) / 31 <= LP_THREADS * 4 &&
+  if (split && o.ts_begin > 0 && (one_win || ns_force == 32) && (o.ts_begin + 30) / 31 <= LP_THREADS * 4 &&
       o.V - o.ts_begin <= LP_THREADS * 4) {
     if (fused) {
       k_logit_part<32, 4, true><<<dim3(rows, 32), LP_THREADS, 0, st>>>(logits, ldl, s, o);

@@ -766,7 +766,9 @@ struct Ctx : public wh_ctx {
   }
 
   // R rows of x_d (embeddings in, residual stream out); on exit xn_d holds the final
-  // decoder LayerNorm of every row (decoder.py:316).
+  // decoder LayerNorm of every row (decoder.py:316) — except on the k_proj1 path
+  // (dec_layers_p1), which leaves final_x set instead: vocab() computes that LayerNorm
+  // in its prologue.
   int dec_layers(int R, const int* rw, const int* rs, const int* rp, int ancG, int nwin, const int* wr0, const int* wnr,
                  const int* wsl, float* aqk, const int* qkmap, int qkrows, bool step = false) {
     const int n = ns;
@@ -775,7 +777,7 @@ struct Ctx : public wh_ctx {
     const bool skinny = step && R <= 128;
     GemmArgs g;
     final_x = nullptr;
-    if (step && !qkmap && p1_active(R))
+    if (step && !qkmap && p1_active(R, nwin))
       return dec_layers_p1(R, rw, rs, rp, ancG, nwin, wr0, wnr, wsl);
     launch_layernorm<T>(x_d, xn_d, dec[0].ln1_g, dec[0].ln1_b, R, n, 1e-5f, nullptr, st);
     for (int l = 0; l < Ld; ++l) {
@@ -852,7 +854,7 @@ struct Ctx : public wh_ctx {
   int layer_projections(int l, int R) {
     const int n = ns;
     auto& e = dec[l];
-    if (p1_active(R)) {
+    if (p1_active(R, cur_nwin)) {
       GemmArgs g;
       g.W = e.wqkv; g.bias = e.bqkv; g.M = R; g.N = 3 * n; g.K = n;
       g.xf32 = x_d; g.ln_g = e.ln1_g; g.ln_b = e.ln1_b; g.ln_eps = 1e-5f;
@@ -888,9 +890,13 @@ struct Ctx : public wh_ctx {
     return 0;
   }
 
-  bool p1_active(int R) const { return p1_enabled() && proj1_supported(R, ns); }
+  // the k_proj1 layers serve exactly one window (its beams, <= P1_RMAX rows): the cut is a
+  // window count, not a row count, so a window's step arithmetic is the same in every
+  // batch of >= 2 windows whatever the beam count (greedy included; batch invariance,
+  // DESIGN.md §2)
+  bool p1_active(int R, int n_win) const { return n_win == 1 && p1_enabled() && proj1_supported(R, ns); }
   std::string step_kernels(int n_win, int group) const override {
-    return std::string("proj=") + (p1_active(n_win * group) ? "k_proj1" : "k_proj") + ",xattn=k_xattn_seg";
+    return std::string("proj=") + (p1_active(n_win * group, n_win) ? "k_proj1" : "k_proj") + ",xattn=k_xattn_seg";
   }
 
   int dec_layers_p1(int R, const int* rw, const int* rs, const int* rp, int ancG, int nwin, const int* wr0,
@@ -966,7 +972,10 @@ struct Ctx : public wh_ctx {
   int vocab(const int* rows_sel, int R, float* out) {
     GemmArgs g;
     g.out_f32 = out; g.ldo = V; g.x_rows = rows_sel;
-    if (final_x && !rows_sel) {
+    // after dec_layers_p1, xn_d does not hold the final LayerNorm: only the prologue path
+    // (every row, no gather) is valid there
+    if (final_x && rows_sel) return fail(-20, "vocab: a row gather after the k_proj1 layers (xn_d not written)");
+    if (final_x) {
       g.xf32 = final_x; g.ln_g = ln_g; g.ln_b = ln_b; g.ln_eps = 1e-5f;
     }
     return gemm(xn_d, ns, E, nullptr, R, V, ns, EPI_F32_COLS, g);

@@ -122,11 +122,11 @@ def _split_segments(tokenizer, result: DecodingResult, seek: int, time_offset: f
 def _check_fp16(model: "Whisper", fp16: bool):
     """transcribe.py:131-140 picks the compute dtype from ``fp16``; here the precision is
     fixed when the context is created (``load_model(..., dtype=)``).  fp16=True on an
-    fp32 context falls back to fp32 with the reference's warning; fp16=False on an fp16
-    context cannot be honoured and raises instead of silently computing in fp16."""
-    if fp16 and model.dtype == "fp32":
-        warnings.warn("FP16 requested but the model was loaded with dtype='fp32'; using FP32 instead")
-    elif not fp16 and model.dtype != "fp32":
+    fp32 context computes in fp32 without a warning (the reference warns only on CPU,
+    and this fork has that warning commented out, reference transcribe.py:136);
+    fp16=False on an fp16 context cannot be honoured and raises instead of silently
+    computing in fp16."""
+    if not fp16 and model.dtype != "fp32":
         raise ValueError("fp16=False needs a context loaded with dtype='fp32' "
                          "(load_model(..., dtype='fp32')); this one computes in fp16")
 
