@@ -52,9 +52,11 @@ _spec.loader.exec_module(syn)
 N_SAMPLES = ref_audio.N_SAMPLES
 
 
-def build_ref_model(name: str, seed: int = 0):
+def build_ref_model(name: str, seed: int = 0, eot_scale=None):
     dims = syn.MODEL_DIMS[name]
     sd = syn.synthetic_state_dict(dims, seed)
+    if eot_scale is not None:
+        syn.scale_eot_embedding(sd, dims, eot_scale)
     model = Whisper(ModelDimensions(**dims), False, name)
     ref_keys = set(model.state_dict().keys())
     assert ref_keys == set(sd.keys()), (ref_keys ^ set(sd.keys()))
@@ -213,6 +215,83 @@ def prefix_goldens(names=("micro", "tiny.en")):
         res[name] = dict(seed=0, audio_seed=1, cases=out)
         del model
     with open(os.path.join(OUT, "prefix.json"), "w") as f:
+        json.dump(res, f, indent=0)
+
+
+class FinalizeRecorder:
+    """Wraps BeamSearchDecoder.finalize (decoding.py:411-431) to record the candidates the
+    ranker sees: their lengths after trimming at EOT and their summed log-probabilities
+    (so a test can tell whether length_penalty had a choice to make)."""
+
+    def __init__(self):
+        self.cands = []
+        self._orig = ref_decoding.BeamSearchDecoder.finalize
+        rec = self
+
+        def finalize(this, preceding_tokens, sum_logprobs):
+            toks, lps = rec._orig(this, preceding_tokens, sum_logprobs)
+            # [untrimmed length (sot sequence .. EOT), summed log-probability], in the
+            # finished set's insertion order
+            rec.cands.append([[len(t.tolist()), float(lp)] for t, lp in zip(toks[0], lps[0])])
+            return toks, lps
+
+        ref_decoding.BeamSearchDecoder.finalize = finalize
+
+    def close(self):
+        ref_decoding.BeamSearchDecoder.finalize = self._orig
+
+
+BEAM_OPTION_CASES = {
+    # decoding.py:339-345: max_candidates = round(beam_size * patience) (Python rounds half to even)
+    "patience2": dict(beam_size=5, patience=2.0),
+    "patience0.5": dict(beam_size=5, patience=0.5),      # round(2.5) = 2
+    "beam3_patience1.5": dict(beam_size=3, patience=1.5),  # round(4.5) = 4
+    # decoding.py:223-240: score = sum_logprob / ((5 + len) / 6) ** length_penalty
+    "lp0.0": dict(beam_size=5, length_penalty=0.0),
+    "lp0.6": dict(beam_size=5, length_penalty=0.6),
+    "lp1.0": dict(beam_size=5, length_penalty=1.0),
+    "patience2_lp0.6": dict(beam_size=5, patience=2.0, length_penalty=0.6),
+    "default": dict(beam_size=5),
+}
+
+
+# With the seeded random weights EOT never wins a natural decode (every candidate runs to
+# sample_len, so patience and length_penalty have nothing to choose between).  Scaling the
+# EOT row of the token embedding (= its logit, decoder.py:319-320) makes EOT compete:
+# these factors give finished candidates of many lengths (micro 8-22 tokens, tiny.en 5-117)
+# and a length_penalty that changes the chosen candidate (micro).
+BEAM_OPTION_EOT_SCALE = {"micro": -3.0, "tiny.en": 3.3}
+
+
+def beam_option_goldens(names=("micro", "tiny.en"), audio_seeds=(1, 2, 3)):
+    """Non-default beam options: natural-mode decodes (EOT allowed)
+    of seeded 30 s windows with patience and length_penalty, tokens / avg_logprob /
+    no_speech_prob plus the finished candidates the ranker chose from, on the seeded
+    weights with the EOT embedding row scaled (BEAM_OPTION_EOT_SCALE)."""
+    res = {}
+    for name in names:
+        model, _ = build_ref_model(name, eot_scale=BEAM_OPTION_EOT_SCALE[name])
+        dims = syn.MODEL_DIMS[name]
+        per_seed = {}
+        for aseed in audio_seeds:
+            audio = syn.synthetic_audio(30.0, seed=aseed)
+            mel = ref_audio.log_mel_spectrogram(audio, dims["n_mels"], padding=N_SAMPLES)
+            seg = ref_audio.pad_or_trim(mel[:, :3000], 3000)
+            out = {}
+            for key, kw in BEAM_OPTION_CASES.items():
+                t0 = time.time()
+                rec = FinalizeRecorder()
+                r = refw.decode(model, seg, ref_decoding.DecodingOptions(temperature=0.0, language="en", fp16=False,
+                                                                         **kw))
+                rec.close()
+                out[key] = dict(options=kw, tokens=[int(t) for t in r.tokens], avg_logprob=float(r.avg_logprob),
+                                no_speech_prob=float(r.no_speech_prob), candidates=rec.cands[0])
+                print(f"[{name}] seed {aseed} {key}: {len(r.tokens)} tok, {len(rec.cands[0])} candidates "
+                      f"{sorted(c[0] for c in rec.cands[0])} {time.time()-t0:.1f}s", flush=True)
+            per_seed[str(aseed)] = out
+        res[name] = dict(seed=0, eot_scale=BEAM_OPTION_EOT_SCALE[name], audio_seeds=list(audio_seeds), cases=per_seed)
+        del model
+    with open(os.path.join(OUT, "beam_options.json"), "w") as f:
         json.dump(res, f, indent=0)
 
 
@@ -563,6 +642,8 @@ def main(argv):
             asset_export()
         elif w == "prefix":
             prefix_goldens()
+        elif w == "beam_options":
+            beam_option_goldens()
         elif w.endswith("_steps_mixed"):
             step_goldens_mixed(w[:-len("_steps_mixed")])
         elif w.endswith("_words_beam"):

@@ -254,6 +254,9 @@ class Result:
     avg_logprob: float
     no_speech_prob: float
     all_logits_first: Optional[torch.Tensor] = None
+    # beam: the candidates the ranker chose from, [untrimmed length, sum_logprob] in the
+    # finished set's order (BeamSearchDecoder.finalize, decoding.py:411-431)
+    candidates: Optional[List[List[float]]] = None
 
 
 def _suppress_list(opts: Options, st: SpecialTokens) -> List[int]:
@@ -406,7 +409,8 @@ def decode(model: OracleWhisper, mel: torch.Tensor, opts: Options, st: Optional[
         sc = [lp_ / ((5 + n) / 6) ** opts.length_penalty for lp_, n in zip(cand_lp, lens)]
     best = int(np.argmax(sc))
     toks = trimmed[best]
-    return Result(toks, cand_lp[best], cand_lp[best] / (len(toks) + 1), no_speech)
+    return Result(toks, cand_lp[best], cand_lp[best] / (len(toks) + 1), no_speech,
+                  candidates=[[len(c), lp_] for c, lp_ in zip(cands, cand_lp)] if beam else None)
 
 
 # ----------------------------------------------------------------------------- transcribe

@@ -88,6 +88,30 @@ def test_micro_transcribe(micro, run):
         assert a["avg_logprob"] == pytest.approx(b["avg_logprob"], abs=1e-4)
 
 
+@pytest.mark.parametrize("name", ["micro", "tiny.en"])
+def test_beam_options(name):
+    """patience / length_penalty (decoding.py:223-240, 334-345, 400-431) against the
+    reference's natural-mode decodes on the EOT-scaled seeded weights
+    (tests/golden/beam_options.json, oracle/gen_golden.py beam_option_goldens): chosen
+    tokens, avg_logprob, and every finished candidate (length, summed log-probability)."""
+    with open(os.path.join(GOLDEN, "beam_options.json")) as f:
+        gb = json.load(f)[name]
+    dims = S.MODEL_DIMS[name]
+    sd = S.synthetic_state_dict(dims, gb["seed"])
+    S.scale_eot_embedding(sd, dims, gb["eot_scale"])
+    model = R.OracleWhisper(dims, sd)
+    for aseed in gb["audio_seeds"][:1 if name == "tiny.en" else None]:
+        audio = S.synthetic_audio(30.0, seed=aseed)
+        mel = R.pad_or_trim(R.log_mel_spectrogram(audio, dims["n_mels"], padding=R.N_SAMPLES)[:, :3000])
+        xa = model.encode(mel)
+        for key, case in gb["cases"][str(aseed)].items():
+            res = R.decode(model, mel, R.Options(**case["options"]), xa=xa)
+            assert res.tokens == case["tokens"], (aseed, key)
+            assert res.avg_logprob == pytest.approx(case["avg_logprob"], abs=1e-4), (aseed, key)
+            assert [c[0] for c in res.candidates] == [c[0] for c in case["candidates"]], (aseed, key)
+            np.testing.assert_allclose([c[1] for c in res.candidates], [c[1] for c in case["candidates"]], atol=1e-3)
+
+
 # ----------------------------------------------------------------------------- timing.py
 def test_dtw_oracle_against_reference():
     """oracle/ref_timing.dtw_cpu vs the reference's dtw_cpu outputs (dtw.npz): planted

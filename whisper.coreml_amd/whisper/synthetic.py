@@ -133,6 +133,16 @@ def synthetic_state_dict(dims: Dict[str, int], seed: int = 0) -> Dict[str, np.nd
     return {k: _tensor(k, shp, seed) for k, shp in state_dict_shapes(dims).items()}
 
 
+def scale_eot_embedding(sd: Dict[str, np.ndarray], dims: Dict[str, int], scale: float) -> None:
+    """Multiplies the EOT row of the decoder token embedding by ``scale`` in place (fp32).
+    With the seeded random weights EOT never wins a natural decode; scaling its row (its
+    logit is x . E[eot], reference decoder.py:319-320) makes candidates finish at many
+    lengths — the test setting for patience / length_penalty (tests/golden/beam_options.json)."""
+    eot = 50257 if dims["n_vocab"] >= 51865 else 50256
+    E = sd["decoder.token_embedding.weight"]
+    E[eot] = (E[eot] * np.float32(scale)).astype(np.float32)
+
+
 def state_dict_checksum(sd: Dict[str, np.ndarray]) -> float:
     """Order-independent float64 checksum used to pin generator determinism."""
     tot = 0.0
