@@ -413,6 +413,9 @@ def main():
         model.ctx.token_ms(reset=True)
         model.ctx.decode_steps(t1.sample_len)
         tk1 = model.ctx.token_ms(reset=True)
+        # the step graph alone, on a live window (after decode_steps the window is done and
+        # the selection / merge would return early): begin the batch again, then 20 replays
+        model.ctx.decode_begin(t1.wh_opts(), [t1.initial_tokens], [t1.sot_index])
         step1 = model.ctx.time_stage(0, 20)
         latency = {"p50_token_ms_1window": round(float(np.median(tk1)), 4), "step_graph_ms_1window": round(step1, 4),
                    "step_bytes_1window": decoder_step_bytes(dims, 1, args.beam, mean_ctx),

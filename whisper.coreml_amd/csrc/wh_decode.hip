@@ -297,6 +297,191 @@ __global__ __launch_bounds__(LR_THREADS) void k_logit_rows(float* __restrict__ l
   }
 }
 
+// ------------------------------------------------------------ candidate merge of a window
+// BeamSearchDecoder.update's bookkeeping (decoding.py:350-409) / GreedyDecoder.update
+// (:304-320) for window w, by NT threads: a 256-thread k_merge workgroup, or the 512
+// threads of the k_logit_part workgroup whose row combine completed the window (the merge
+// folded into the selection launch, round 4).  SC1: the candidates were written in the
+// same launch by other CUs (write-through stores, counted on s.lpw_cnt): read them with sc1
+// loads (cdna_hip_programming.md §6 Guideline 16 R1).
+constexpr int MG_MAXG = 8;
+constexpr int MG_MAXCTX = 449;
+struct MergeLds {
+  int oh[MG_MAXG][MG_MAXCTX];
+  int oa[MG_MAXG][MG_MAXCTX];
+  int src[MG_MAXG], tok[MG_MAXG], fsrc[MG_MAXG * KC];
+  float fsc[MG_MAXG * KC];
+  int nfin_new;
+  int etok[MG_MAXG];  // each row's input token for the next step
+  float csc[MG_MAXG * KC];
+  int csrc[MG_MAXG * KC], ctok[MG_MAXG * KC], rk[MG_MAXG * KC];
+};
+// the next step's input rows of window w (k_embed's arithmetic: x = E[tok] + P[pos] in
+// fp32, pos = min(length - 1, pmax)); newtok[b]: row b's token at pos (passed from
+// registers / LDS: that history word may have been written by another lane of this
+// workgroup, and a plain reload could hit a stale L1 copy of its line)
+template <typename T, int NT>
+__device__ void merge_embed_rows(const MergeEmbed& em, int w, int G, int pos, const int* newtok, int tid) {
+  const T* E = reinterpret_cast<const T*>(em.E);
+  const T* P = reinterpret_cast<const T*>(em.P);
+  const int n4 = em.n / 4;
+  for (int i = tid; i < G * n4; i += NT) {
+    const int b = i / n4, c = 4 * (i - b * n4), r = w * G + b;
+    const float4_t e = load4f(E + (int64_t)newtok[b] * em.n + c), p = load4f(P + (int64_t)pos * em.n + c);
+    const float4_t v = e + p;
+    store4(em.x + (int64_t)r * em.n + c, v[0], v[1], v[2], v[3]);
+  }
+  if (tid < G) em.row_pos[w * G + tid] = pos;
+}
+template <int NT>
+__device__ void merge_embed(const MergeEmbed& em, int w, int G, int pos, const int* newtok, int tid) {
+  if (em.half) merge_embed_rows<half_t, NT>(em, w, G, pos, newtok, tid);
+  else merge_embed_rows<float, NT>(em, w, G, pos, newtok, tid);
+}
+
+template <int NT, bool SC1>
+__device__ __forceinline__ void merge_window(const DecState& s, const DecOpts& o, const MergeEmbed& em, int w, int tid, MergeLds& L) {
+  const int G = s.G, len = s.len[w], sb = s.sample_begin[w];
+  int* hist = s.hist + (int64_t)w * G * s.hctx;
+  int* anc = s.anc + (int64_t)w * G * s.ctx;
+  if (s.done[w]) {
+    // finished windows keep recomputing a valid row (as k_embed did): nothing of theirs
+    // is written in this kernel, so the history words are read as they stand
+    if (em.x) {
+      const int pos = min(len - 1, em.pmax);
+      if (tid < G) L.etok[tid] = hist[tid * s.hctx + pos];
+      __syncthreads();
+      merge_embed<NT>(em, w, G, pos, L.etok, tid);
+    }
+    return;
+  }
+  const auto rsv = wt_rsrc(s.cand_val), rsi = wt_rsrc(s.cand_idx);
+  auto cval = [&](int i) -> float {
+    if constexpr (SC1) return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsv, i * 4, 0, 16));
+    else return s.cand_val[i];
+  };
+  auto cidx = [&](int i) -> int {
+    if constexpr (SC1) return (int)__builtin_amdgcn_raw_buffer_load_b32(rsi, i * 4, 0, 16);
+    else return s.cand_idx[i];
+  };
+  if (!o.beam) {
+    if (tid < G) {
+      const int r = w * G + tid;
+      const int last = hist[tid * s.hctx + len - 1];
+      int t = cidx(r * KC);
+      if (last == o.eot) t = o.eot;
+      else s.sum_lp[r] += cval(r * KC);
+      hist[tid * s.hctx + len] = t;
+      L.tok[tid] = t;
+    }
+    __syncthreads();
+    if (tid == 0) {
+      int all_eot = 1;
+      for (int b = 0; b < G; ++b) all_eot &= (L.tok[b] == o.eot);
+      s.len[w] = len + 1;
+      const int st = s.step[w] + 1;
+      s.step[w] = st;
+      if (all_eot || len + 1 > o.n_ctx || st >= o.sample_len) s.done[w] = 1;
+    }
+    if (em.x) {
+      const int pos = min(len, em.pmax);  // the new length is len + 1
+      if (tid < G) L.etok[tid] = pos == len ? L.tok[tid] : hist[tid * s.hctx + pos];  // pos < len: not written here
+      __syncthreads();
+      merge_embed<NT>(em, w, G, pos, L.etok, tid);
+    }
+    return;
+  }
+  // stage old histories / ancestry
+  for (int i = tid; i < G * len; i += NT) {
+    const int b = i / len, p = i - b * len;
+    L.oh[b][p] = hist[b * s.hctx + p];
+    int a = (p < s.ctx) ? anc[b * s.ctx + p] : 0;
+    if (p == len - 1 && p >= sb) a = b;  // this step's KV of beam b was written in slot b
+    L.oa[b][p] = a;
+  }
+  // candidates in insertion order: beam-major, top-k order (decoding.py:366-373);
+  // at the first update all beams are identical: dict keys collapse onto beam 0's
+  // candidates with the source of the last duplicate (G-1).  Gathered by one lane
+  // each (independent loads), then ranked from LDS.
+  const bool first = (len == sb);
+  const int nbeams = first ? 1 : G;
+  const int nc = nbeams * (G + 1);
+  for (int c0 = tid; c0 < nc; c0 += NT) {
+    const int b = c0 / (G + 1), k = c0 - b * (G + 1), r = w * G + b;
+    L.csc[c0] = s.sum_lp[r] + cval(r * KC + k);
+    L.ctok[c0] = cidx(r * KC + k);
+    L.csrc[c0] = first ? (G - 1) : b;
+  }
+  __syncthreads();
+  // stable descending sort by rank (ties keep insertion order), then the walk of
+  // decoding.py:375-386 in closed form: the candidate at rank q is taken iff fewer
+  // than G non-EOT candidates rank above it; a non-EOT one becomes beam
+  // #(non-EOT above), an EOT one finished sequence #(EOT above).  One lane per
+  // candidate, no serial loop.
+  for (int c0 = tid; c0 < nc; c0 += NT) {
+    const float sc = L.csc[c0];
+    int q = 0;
+    for (int c = 0; c < nc; ++c) q += (L.csc[c] > sc) || (L.csc[c] == sc && c < c0);
+    L.rk[c0] = q;
+  }
+  if (tid == 0) L.nfin_new = 0;
+  __syncthreads();
+  for (int c0 = tid; c0 < nc; c0 += NT) {
+    const int q = L.rk[c0];
+    int ne = 0, ee = 0;  // non-EOT / EOT candidates ranked above
+    for (int c = 0; c < nc; ++c)
+      if (L.rk[c] < q) {
+        if (L.ctok[c] == o.eot) ++ee;
+        else ++ne;
+      }
+    if (ne < G) {
+      if (L.ctok[c0] == o.eot) {
+        L.fsc[ee] = L.csc[c0];
+        L.fsrc[ee] = L.csrc[c0];
+        atomicAdd(&L.nfin_new, 1);
+      } else {
+        L.src[ne] = L.csrc[c0];
+        L.tok[ne] = L.ctok[c0];
+        s.sum_lp[w * G + ne] = L.csc[c0];
+      }
+    }
+  }
+  __syncthreads();
+  // new histories / ancestry
+  for (int i = tid; i < G * (len + 1); i += NT) {
+    const int j = i / (len + 1), p = i - j * (len + 1);
+    hist[j * s.hctx + p] = (p < len) ? L.oh[L.src[j]][p] : L.tok[j];
+    if (p < len && p < s.ctx) anc[j * s.ctx + p] = L.oa[L.src[j]][p];
+  }
+  // finished sequences (already in descending order)
+  int fin0 = s.fin_n[w];
+  const int nadd = min(L.nfin_new, max(0, s.maxc - fin0));
+  for (int i = tid; i < nadd * (len + 1); i += NT) {
+    const int f = i / (len + 1), p = i - f * (len + 1);
+    s.fin_tok[((int64_t)w * s.maxc + fin0 + f) * s.hctx + p] = (p < len) ? L.oh[L.fsrc[f]][p] : o.eot;
+  }
+  if (tid < nadd) {
+    s.fin_score[w * s.maxc + fin0 + tid] = L.fsc[tid];
+    s.fin_len[w * s.maxc + fin0 + tid] = len + 1;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    const int fn = fin0 + nadd;
+    s.fin_n[w] = fn;
+    s.len[w] = len + 1;
+    const int st = s.step[w] + 1;
+    s.step[w] = st;
+    if (fn >= s.maxc || len + 1 > o.n_ctx || st >= o.sample_len) s.done[w] = 1;
+  }
+  if (em.x) {
+    // row j's new history is oh[src[j]][0, len) + tok[j]: its input token from LDS
+    const int pos = min(len, em.pmax);
+    if (tid < G) L.etok[tid] = pos == len ? L.tok[tid] : L.oh[L.src[tid]][pos];
+    __syncthreads();
+    merge_embed<NT>(em, w, G, pos, L.etok, tid);
+  }
+}
+
 // ---------------------------------------------------------------- split selection
 // The same selection with each row's vocabulary in NS slices, one 512-thread
 // workgroup per (row, slice): slices 0..NS-2 split the text ids [0, ts_begin),
@@ -344,7 +529,7 @@ __device__ __forceinline__ void wave_argbest(float& v, int& idx) {
   }
 }
 
-template <int NS>
+template <int NS, bool WT>
 __device__ __forceinline__ void lp_combine(const LPRec* rec, int r, const DecState& s, const DecOpts& o, int lane);
 
 // Two barriers per workgroup: (1) after the history scan (last sampled timestamp), (2)
@@ -352,10 +537,20 @@ __device__ __forceinline__ void lp_combine(const LPRec* rec, int r, const DecSta
 // argbest / Gumbel best); wave 0 then merges the 8 wave results and writes the record.
 // The slice's logits and suppress words are loaded first, before the history, so their
 // round trip overlaps it.
-template <int NS, int LP_EPT, bool FUSED>
+//
+// MERGE (with FUSED): the candidates of the row combine are stored write-through and counted
+// on the window's counter (s.lpw_cnt); the combine completing the window tells its
+// workgroup, whose 8 waves then run the window's candidate merge (k_merge folded in:
+// merge_window<512, sc1 candidate loads>).  A finished window's rows are re-embedded by
+// its first row's first slice.
+template <int NS, int LP_EPT, bool FUSED, bool MERGE = false>
 __global__ __launch_bounds__(LP_THREADS) WH_LP_ATTR void k_logit_part(float* __restrict__ logits, int ldl, DecState s,
-                                                           DecOpts o) {
+                                                           DecOpts o, MergeEmbed em) {
+  static_assert(FUSED || !MERGE, "the merge rides on the fused combine");
   constexpr int NWV = LP_THREADS / 64;
+  __shared__ __attribute__((aligned(16))) char mlds_raw[MERGE ? sizeof(MergeLds) : 4];
+  MergeLds& mlds = *reinterpret_cast<MergeLds*>(mlds_raw);
+  __shared__ int s_go;
   __shared__ int pm_w[NWV], pt_w[NWV];
   __shared__ float wmx[NWV], wse[NWV], wv_v[NWV][KC], wg_v[NWV], wg_x[NWV];
   __shared__ int wv_i[NWV][KC], wg_i[NWV];
@@ -375,7 +570,11 @@ __global__ __launch_bounds__(LP_THREADS) WH_LP_ATTR void k_logit_part(float* __r
     sw[u] = o.suppress ? o.suppress[ic >> 5] : 0u;
   }
   const int done = s.done[w], len = s.len[w], sb = s.sample_begin[w];
-  if (done) return;
+  if (done) {
+    if constexpr (MERGE)
+      if (j == 0 && r == w * s.G) merge_window<LP_THREADS, false>(s, o, em, w, tid, mlds);
+    return;
+  }
   // 2. history facts (decoding.py:503-508): the last timestamp token of the sampled
   // part (len - sb <= 448 < LP_THREADS: one position per thread) and the last two tokens
   const int* hist = s.hist + (int64_t)r * s.hctx;
@@ -454,12 +653,13 @@ __global__ __launch_bounds__(LP_THREADS) WH_LP_ATTR void k_logit_part(float* __r
   // record's sc1 stores drained (vmcnt(0)), a relaxed agent add on the row's counter; the
   // wave drawing NS - 1 re-arms it and reads the NS records with sc1 loads into LDS
   __shared__ __attribute__((aligned(16))) float recs[FUSED ? NS * LP_REC : 4];
-  auto arrive_and_combine = [&]() {
+  // (wave 0) returns true when this combine completed the window (MERGE)
+  auto arrive_and_combine = [&]() -> bool {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     int ticket = 0;
     if (lane == 0) ticket = __hip_atomic_fetch_add(s.lp_cnt + r, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     ticket = __shfl(ticket, 0, 64);
-    if (ticket != NS - 1) return;
+    if (ticket != NS - 1) return false;
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // no instruction: keeps the loads below the add
     if (lane == 0) __hip_atomic_store(s.lp_cnt + r, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     constexpr int N4 = NS * LP_REC / 4, PER = (N4 + 63) / 64;
@@ -471,7 +671,25 @@ __global__ __launch_bounds__(LP_THREADS) WH_LP_ATTR void k_logit_part(float* __r
     for (int k = 0; k < PER; ++k)
       if (lane + 64 * k < N4) reinterpret_cast<float4_t*>(recs)[lane + 64 * k] = v[k];
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // one wave: its own LDS writes, no barrier
-    lp_combine<NS>(reinterpret_cast<const LPRec*>(recs), r, s, o, lane);
+    lp_combine<NS, MERGE>(reinterpret_cast<const LPRec*>(recs), r, s, o, lane);
+    if constexpr (!MERGE) return false;
+    // the row's candidates (sc1 stores) drained, then the window's arrival
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    int wt = 0;
+    if (lane == 0) wt = __hip_atomic_fetch_add(s.lpw_cnt + w, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    wt = __shfl(wt, 0, 64);
+    if (wt != s.G - 1) return false;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // no instruction: keeps the loads below the add
+    if (lane == 0) __hip_atomic_store(s.lpw_cnt + w, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return true;
+  };
+  // MERGE: wave 0 tells the workgroup whether it merges the window
+  auto finish = [&](bool go) {
+    if constexpr (MERGE) {
+      if (wv == 0 && lane == 0) s_go = go;
+      __syncthreads();
+      if (s_go) merge_window<LP_THREADS, true>(s, o, em, w, tid, mlds);
+    }
   };
   const int need = s.G + 1;
   if (!o.beam) {
@@ -519,64 +737,69 @@ __global__ __launch_bounds__(LP_THREADS) WH_LP_ATTR void k_logit_part(float* __r
     }
   }
   __syncthreads();
-  if (wv != 0) return;
-  // 4. wave 0 merges the NWV wave results
-  float MX = -INFINITY;
+  if (!MERGE && wv != 0) return;
+  bool go = false;
+  if (wv == 0) {
+    // 4. wave 0 merges the NWV wave results
+    float MX = -INFINITY;
 #pragma unroll
-  for (int k = 0; k < NWV; ++k) MX = fmaxf(MX, wmx[k]);
-  float SE = 0.f;
-  if (MX > -INFINITY) {
+    for (int k = 0; k < NWV; ++k) MX = fmaxf(MX, wmx[k]);
+    float SE = 0.f;
+    if (MX > -INFINITY) {
 #pragma unroll
-    for (int k = 0; k < NWV; ++k)
-      if (wmx[k] > -INFINITY) SE += wse[k] * __expf(wmx[k] - MX);
-  }
-  if (!o.beam) {
-    float bv = lane < NWV ? wv_v[lane][0] : -INFINITY, gv = lane < NWV ? wg_v[lane] : -INFINITY;
-    int bi = lane < NWV ? wv_i[lane][0] : 0x7fffffff, gi = lane < NWV ? wg_i[lane] : 0x7fffffff;
-    const float myx = lane < NWV ? wg_x[lane] : -INFINITY;
-    const int mine = gi;
-    wave_argbest(bv, bi);
-    wave_argbest(gv, gi);
-    const unsigned long long own = __ballot(mine == gi && gi != 0x7fffffff);
-    const float gx = own ? __shfl(myx, __ffsll((long long)own) - 1, 64) : -INFINITY;
-    if (lane == 0) {
-      wt_rec(rec_off + offsetof(LPRec, mx), MX); wt_rec(rec_off + offsetof(LPRec, se), SE);
-      wt_rec(rec_off + offsetof(LPRec, bv), bv); wt_rec(rec_off + offsetof(LPRec, bi), __builtin_bit_cast(float, bi));
-      wt_rec(rec_off + offsetof(LPRec, gv), gv); wt_rec(rec_off + offsetof(LPRec, gi), __builtin_bit_cast(float, gi));
-      wt_rec(rec_off + offsetof(LPRec, gx), gi != 0x7fffffff ? gx : -INFINITY);
+      for (int k = 0; k < NWV; ++k)
+        if (wmx[k] > -INFINITY) SE += wse[k] * __expf(wmx[k] - MX);
     }
-    if constexpr (FUSED) arrive_and_combine();
-    return;
-  }
-  // beam: each lane holds up to two wave candidates (NWV * need <= 72), sorted within
-  // the lane; `need` wave-level rounds take the best remaining head
-  const int c0 = lane, c1 = lane + 64, nc = NWV * need;
-  float a0 = -INFINITY, a1 = -INFINITY;
-  int i0 = 0x7fffffff, i1 = 0x7fffffff;
-  if (c0 < nc) { a0 = wv_v[c0 / need][c0 % need]; i0 = wv_i[c0 / need][c0 % need]; }
-  if (c1 < nc) { a1 = wv_v[c1 / need][c1 % need]; i1 = wv_i[c1 / need][c1 % need]; }
-  if (better(a1, i1, a0, i0)) {
-    const float tv = a0; const int ti = i0;
-    a0 = a1; i0 = i1; a1 = tv; i1 = ti;
-  }
-  for (int q = 0; q < need; ++q) {
-    float bv = a0;
-    int bi = i0;
-    wave_argbest(bv, bi);
-    if (bi == i0 && bi != 0x7fffffff) { a0 = a1; i0 = i1; a1 = -INFINITY; i1 = 0x7fffffff; }
-    if (lane == 0) {
-      wt_rec(rec_off + offsetof(LPRec, tv) + 4 * q, bv);
-      wt_rec(rec_off + offsetof(LPRec, ti) + 4 * q, __builtin_bit_cast(float, bi));
+    if (!o.beam) {
+      float bv = lane < NWV ? wv_v[lane][0] : -INFINITY, gv = lane < NWV ? wg_v[lane] : -INFINITY;
+      int bi = lane < NWV ? wv_i[lane][0] : 0x7fffffff, gi = lane < NWV ? wg_i[lane] : 0x7fffffff;
+      const float myx = lane < NWV ? wg_x[lane] : -INFINITY;
+      const int mine = gi;
+      wave_argbest(bv, bi);
+      wave_argbest(gv, gi);
+      const unsigned long long own = __ballot(mine == gi && gi != 0x7fffffff);
+      const float gx = own ? __shfl(myx, __ffsll((long long)own) - 1, 64) : -INFINITY;
+      if (lane == 0) {
+        wt_rec(rec_off + offsetof(LPRec, mx), MX); wt_rec(rec_off + offsetof(LPRec, se), SE);
+        wt_rec(rec_off + offsetof(LPRec, bv), bv); wt_rec(rec_off + offsetof(LPRec, bi), __builtin_bit_cast(float, bi));
+        wt_rec(rec_off + offsetof(LPRec, gv), gv); wt_rec(rec_off + offsetof(LPRec, gi), __builtin_bit_cast(float, gi));
+        wt_rec(rec_off + offsetof(LPRec, gx), gi != 0x7fffffff ? gx : -INFINITY);
+      }
+      if constexpr (FUSED) go = arrive_and_combine();
+    } else {
+      // beam: each lane holds up to two wave candidates (NWV * need <= 72), sorted within
+      // the lane; `need` wave-level rounds take the best remaining head
+      const int c0 = lane, c1 = lane + 64, nc = NWV * need;
+      float a0 = -INFINITY, a1 = -INFINITY;
+      int i0 = 0x7fffffff, i1 = 0x7fffffff;
+      if (c0 < nc) { a0 = wv_v[c0 / need][c0 % need]; i0 = wv_i[c0 / need][c0 % need]; }
+      if (c1 < nc) { a1 = wv_v[c1 / need][c1 % need]; i1 = wv_i[c1 / need][c1 % need]; }
+      if (better(a1, i1, a0, i0)) {
+        const float tv = a0; const int ti = i0;
+        a0 = a1; i0 = i1; a1 = tv; i1 = ti;
+      }
+      for (int q = 0; q < need; ++q) {
+        float bv = a0;
+        int bi = i0;
+        wave_argbest(bv, bi);
+        if (bi == i0 && bi != 0x7fffffff) { a0 = a1; i0 = i1; a1 = -INFINITY; i1 = 0x7fffffff; }
+        if (lane == 0) {
+          wt_rec(rec_off + offsetof(LPRec, tv) + 4 * q, bv);
+          wt_rec(rec_off + offsetof(LPRec, ti) + 4 * q, __builtin_bit_cast(float, bi));
+        }
+      }
+      if (lane == 0) { wt_rec(rec_off + offsetof(LPRec, mx), MX); wt_rec(rec_off + offsetof(LPRec, se), SE); }
+      if constexpr (FUSED) go = arrive_and_combine();
     }
-  }
-  if (lane == 0) { wt_rec(rec_off + offsetof(LPRec, mx), MX); wt_rec(rec_off + offsetof(LPRec, se), SE); }
-  if constexpr (FUSED) arrive_and_combine();
+  }  // wave 0
+  finish(go);
 }
 
 // the merge of a row's NS slice records (in LDS, `rec`) by one wave: the timestamp-rule
 // selection between text and timestamps, the normaliser, then argbest / top-(G+1) with one
 // slice per lane (decoding.py:522-531 and the candidate lists of 707-733)
-template <int NS>
+// WT: the candidates are stored write-through (sc1), for the merge in the same launch
+template <int NS, bool WT>
 __device__ __forceinline__ void lp_combine(const LPRec* rec, int r, const DecState& s, const DecOpts& o, int lane) {
   constexpr int TS = NS - 1;
   float m = -INFINITY;
@@ -619,8 +842,13 @@ __device__ __forceinline__ void lp_combine(const LPRec* rec, int r, const DecSta
     const unsigned long long own = __ballot(mine == bi && bi != 0x7fffffff);
     const float wx = own ? __shfl(myx, __ffsll((long long)own) - 1, 64) : -INFINITY;
     if (lane == 0 && bi != 0x7fffffff) {
-      ci[0] = bi;
-      cv[0] = (wx - m) - logS;
+      if constexpr (WT) {
+        wt_store1(wt_rsrc(ci), 0, __builtin_bit_cast(float, bi));
+        wt_store1(wt_rsrc(cv), 0, (wx - m) - logS);
+      } else {
+        ci[0] = bi;
+        cv[0] = (wx - m) - logS;
+      }
     }
     return;
   }
@@ -636,8 +864,13 @@ __device__ __forceinline__ void lp_combine(const LPRec* rec, int r, const DecSta
     wave_argbest(bv, bi);
     if (bi == hi && bi != 0x7fffffff) ++hd;
     if (lane == 0) {
-      cv[q] = (bv - m) - logS;
-      ci[q] = bi;
+      if constexpr (WT) {
+        wt_store1(wt_rsrc(cv), 4 * q, (bv - m) - logS);
+        wt_store1(wt_rsrc(ci), 4 * q, __builtin_bit_cast(float, bi));
+      } else {
+        cv[q] = (bv - m) - logS;
+        ci[q] = bi;
+      }
     }
   }
 }
@@ -661,17 +894,29 @@ __global__ __launch_bounds__(64) void k_logit_combine(DecState s, DecOpts o) {
       if (lane + 64 * k < N4) dst[lane + 64 * k] = v[k];
   }
   __syncthreads();
-  lp_combine<NS>(reinterpret_cast<const LPRec*>(recs), r, s, o, lane);
+  lp_combine<NS, false>(reinterpret_cast<const LPRec*>(recs), r, s, o, lane);
 }
 
-void launch_logit_rows(float* logits, int ldl, const DecState& s, const DecOpts& o, int nwin, hipStream_t st) {
+// the selection of one update; with `em` (launch_select_merge) the fused k_logit_part also
+// runs each window's merge and this returns true
+static bool select_rows(float* logits, int ldl, const DecState& s, const DecOpts& o, int nwin, hipStream_t st,
+                        const MergeEmbed* em) {
   // the sliced selection (k_logit_part + k_logit_combine) unless WHISPER_HIP_LOGIT_SPLIT=0
   // (config 2, turbo one window: 0.380 -> 0.346 ms per token; config 3 unchanged)
   static const bool split = [] {
     const char* e = tune_env("WHISPER_HIP_LOGIT_SPLIT");
     return !(e && e[0] == '0');
   }();
+  // the window's merge in the selection launch unless WHISPER_HIP_LP_MERGE=0 (tuning: k_merge
+  // as its own launch)
+  static const bool fold_merge = [] {
+    const char* e = tune_env("WHISPER_HIP_LP_MERGE");
+    return !(e && e[0] == '0');
+  }();
   const int rows = nwin * s.G;
+  const bool merge = em && fold_merge && s.lpw_cnt && s.G <= MG_MAXG;
+  const MergeEmbed none;
+  const MergeEmbed& e = em ? *em : none;
   // the records merged by the row's last slice (fused) unless WHISPER_HIP_LP_FUSED=0 (tuning:
   // k_logit_combine as its own launch)
   const char* fe = tune_env("WHISPER_HIP_LP_FUSED");
@@ -689,154 +934,52 @@ void launch_logit_rows(float* logits, int ldl, const DecState& s, const DecOpts&
   const bool one_win = nwin == 1;
   if (split && fused && !one_win && ns_force == 16 && o.ts_begin > 0 &&
       (o.ts_begin + 14) / 15 <= LP_THREADS * 8 && o.V - o.ts_begin <= LP_THREADS * 8) {
-    k_logit_part<16, 8, true><<<dim3(rows, 16), LP_THREADS, 0, st>>>(logits, ldl, s, o);
-    return;
+    if (merge) k_logit_part<16, 8, true, true><<<dim3(rows, 16), LP_THREADS, 0, st>>>(logits, ldl, s, o, e);
+    else k_logit_part<16, 8, true><<<dim3(rows, 16), LP_THREADS, 0, st>>>(logits, ldl, s, o, e);
+    return merge;
   }
   if (split && o.ts_begin > 0 && (one_win || ns_force == 32) && (o.ts_begin + 30) / 31 <= LP_THREADS * 4 &&
       o.V - o.ts_begin <= LP_THREADS * 4) {
     if (fused) {
-      k_logit_part<32, 4, true><<<dim3(rows, 32), LP_THREADS, 0, st>>>(logits, ldl, s, o);
-    } else {
-      k_logit_part<32, 4, false><<<dim3(rows, 32), LP_THREADS, 0, st>>>(logits, ldl, s, o);
-      k_logit_combine<32><<<rows, 64, 0, st>>>(s, o);
+      if (merge) k_logit_part<32, 4, true, true><<<dim3(rows, 32), LP_THREADS, 0, st>>>(logits, ldl, s, o, e);
+      else k_logit_part<32, 4, true><<<dim3(rows, 32), LP_THREADS, 0, st>>>(logits, ldl, s, o, e);
+      return merge;
     }
-    return;
+    k_logit_part<32, 4, false><<<dim3(rows, 32), LP_THREADS, 0, st>>>(logits, ldl, s, o, e);
+    k_logit_combine<32><<<rows, 64, 0, st>>>(s, o);
+    return false;
   }
   if (split && o.ts_begin > 0 && (o.ts_begin + 6) / 7 <= LP_THREADS * 16 && o.V - o.ts_begin <= LP_THREADS * 16) {
     if (fused) {
-      k_logit_part<8, 16, true><<<dim3(rows, 8), LP_THREADS, 0, st>>>(logits, ldl, s, o);
-    } else {
-      k_logit_part<8, 16, false><<<dim3(rows, 8), LP_THREADS, 0, st>>>(logits, ldl, s, o);
-      k_logit_combine<8><<<rows, 64, 0, st>>>(s, o);
+      if (merge) k_logit_part<8, 16, true, true><<<dim3(rows, 8), LP_THREADS, 0, st>>>(logits, ldl, s, o, e);
+      else k_logit_part<8, 16, true><<<dim3(rows, 8), LP_THREADS, 0, st>>>(logits, ldl, s, o, e);
+      return merge;
     }
-    return;
+    k_logit_part<8, 16, false><<<dim3(rows, 8), LP_THREADS, 0, st>>>(logits, ldl, s, o, e);
+    k_logit_combine<8><<<rows, 64, 0, st>>>(s, o);
+    return false;
   }
   k_logit_rows<<<nwin * s.G, LR_THREADS, 0, st>>>(logits, ldl, s, o);
+  return false;
+}
+
+void launch_logit_rows(float* logits, int ldl, const DecState& s, const DecOpts& o, int nwin, hipStream_t st) {
+  select_rows(logits, ldl, s, o, nwin, st, nullptr);
 }
 
 // ------------------------------------------------------------ merge (one workgroup per window)
-constexpr int MG_MAXG = 8;
-constexpr int MG_MAXCTX = 449;
-__global__ __launch_bounds__(256) void k_merge(DecState s, DecOpts o) {
-  __shared__ int oh[MG_MAXG][MG_MAXCTX];
-  __shared__ int oa[MG_MAXG][MG_MAXCTX];
-  __shared__ int src[MG_MAXG], tok[MG_MAXG], fsrc[MG_MAXG * KC];
-  __shared__ float fsc[MG_MAXG * KC];
-  __shared__ int nfin_new, completed;
-  const int w = blockIdx.x, tid = threadIdx.x;
-  if (s.done[w]) return;
-  const int G = s.G, len = s.len[w], sb = s.sample_begin[w];
-  int* hist = s.hist + (int64_t)w * G * s.hctx;
-  int* anc = s.anc + (int64_t)w * G * s.ctx;
-  if (!o.beam) {
-    if (tid < G) {
-      const int r = w * G + tid;
-      const int last = hist[tid * s.hctx + len - 1];
-      int t = s.cand_idx[r * KC];
-      if (last == o.eot) t = o.eot;
-      else s.sum_lp[r] += s.cand_val[r * KC];
-      hist[tid * s.hctx + len] = t;
-    }
-    __syncthreads();
-    if (tid == 0) {
-      int all_eot = 1;
-      for (int b = 0; b < G; ++b) all_eot &= (hist[b * s.hctx + len] == o.eot);
-      s.len[w] = len + 1;
-      const int st = s.step[w] + 1;
-      s.step[w] = st;
-      if (all_eot || len + 1 > o.n_ctx || st >= o.sample_len) s.done[w] = 1;
-    }
-    return;
-  }
-  // stage old histories / ancestry
-  for (int i = tid; i < G * len; i += 256) {
-    const int b = i / len, p = i - b * len;
-    oh[b][p] = hist[b * s.hctx + p];
-    int a = (p < s.ctx) ? anc[b * s.ctx + p] : 0;
-    if (p == len - 1 && p >= sb) a = b;  // this step's KV of beam b was written in slot b
-    oa[b][p] = a;
-  }
-  // candidates in insertion order: beam-major, top-k order (decoding.py:366-373);
-  // at the first update all beams are identical: dict keys collapse onto beam 0's
-  // candidates with the source of the last duplicate (G-1).  Gathered by one lane
-  // each (independent loads), then sorted by one lane from LDS.
-  __shared__ float csc[MG_MAXG * KC];
-  __shared__ int csrc[MG_MAXG * KC], ctok[MG_MAXG * KC];
-  const bool first = (len == sb);
-  const int nbeams = first ? 1 : G;
-  const int nc = nbeams * (G + 1);
-  if (tid < nc) {
-    const int b = tid / (G + 1), k = tid - b * (G + 1), r = w * G + b;
-    csc[tid] = s.sum_lp[r] + s.cand_val[r * KC + k];
-    ctok[tid] = s.cand_idx[r * KC + k];
-    csrc[tid] = first ? (G - 1) : b;
-  }
-  __syncthreads();
-  // stable descending sort by rank (ties keep insertion order), then the walk of
-  // decoding.py:375-386 in closed form: the candidate at rank q is taken iff fewer
-  // than G non-EOT candidates rank above it; a non-EOT one becomes beam
-  // #(non-EOT above), an EOT one finished sequence #(EOT above).  One lane per
-  // candidate, no serial loop.
-  __shared__ int rk[MG_MAXG * KC];
-  if (tid < nc) {
-    const float sc = csc[tid];
-    int q = 0;
-    for (int c = 0; c < nc; ++c) q += (csc[c] > sc) || (csc[c] == sc && c < tid);
-    rk[tid] = q;
-  }
-  if (tid == 0) nfin_new = 0;
-  __syncthreads();
-  if (tid < nc) {
-    const int q = rk[tid];
-    int ne = 0, ee = 0;  // non-EOT / EOT candidates ranked above
-    for (int c = 0; c < nc; ++c)
-      if (rk[c] < q) {
-        if (ctok[c] == o.eot) ++ee;
-        else ++ne;
-      }
-    if (ne < G) {
-      if (ctok[tid] == o.eot) {
-        fsc[ee] = csc[tid];
-        fsrc[ee] = csrc[tid];
-        atomicAdd(&nfin_new, 1);
-      } else {
-        src[ne] = csrc[tid];
-        tok[ne] = ctok[tid];
-        s.sum_lp[w * G + ne] = csc[tid];
-      }
-    }
-  }
-  __syncthreads();
-  // new histories / ancestry
-  for (int i = tid; i < G * (len + 1); i += 256) {
-    const int j = i / (len + 1), p = i - j * (len + 1);
-    hist[j * s.hctx + p] = (p < len) ? oh[src[j]][p] : tok[j];
-    if (p < len && p < s.ctx) anc[j * s.ctx + p] = oa[src[j]][p];
-  }
-  // finished sequences (already in descending order)
-  int fin0 = s.fin_n[w];
-  const int nadd = min(nfin_new, max(0, s.maxc - fin0));
-  for (int i = tid; i < nadd * (len + 1); i += 256) {
-    const int f = i / (len + 1), p = i - f * (len + 1);
-    s.fin_tok[((int64_t)w * s.maxc + fin0 + f) * s.hctx + p] = (p < len) ? oh[fsrc[f]][p] : o.eot;
-  }
-  if (tid < nadd) {
-    s.fin_score[w * s.maxc + fin0 + tid] = fsc[tid];
-    s.fin_len[w * s.maxc + fin0 + tid] = len + 1;
-  }
-  __syncthreads();
-  if (tid == 0) {
-    const int fn = fin0 + nadd;
-    s.fin_n[w] = fn;
-    s.len[w] = len + 1;
-    const int st = s.step[w] + 1;
-    s.step[w] = st;
-    if (fn >= s.maxc || len + 1 > o.n_ctx || st >= o.sample_len) s.done[w] = 1;
-  }
+__global__ __launch_bounds__(256) void k_merge(DecState s, DecOpts o, MergeEmbed em) {
+  __shared__ MergeLds L;
+  merge_window<256, false>(s, o, em, blockIdx.x, threadIdx.x, L);
 }
 
-void launch_merge(const DecState& s, const DecOpts& o, int nwin, hipStream_t st) {
-  k_merge<<<nwin, 256, 0, st>>>(s, o);
+void launch_merge(const DecState& s, const DecOpts& o, int nwin, hipStream_t st, const MergeEmbed& em) {
+  k_merge<<<nwin, 256, 0, st>>>(s, o, em);
+}
+
+void launch_select_merge(float* logits, int ldl, const DecState& s, const DecOpts& o, int nwin, hipStream_t st,
+                         const MergeEmbed& em) {
+  if (!select_rows(logits, ldl, s, o, nwin, st, &em)) launch_merge(s, o, nwin, st, em);
 }
 
 // ------------------------------------------------------------ per-step ABI state updates

@@ -63,6 +63,9 @@ struct GemmArgs {
   const float* res_slab = nullptr;
   const float* res_bias = nullptr;
   float* x_out = nullptr;
+  // k_proj EPI_PARTIAL in an fp16 context: store the split-K slabs as fp16 (out_f32 then
+  // holds half_t elements; wh_kernels.h slab consumers take slab_half = 1)
+  int slab_half = 0;
 };
 
 template <typename T, int EPI>

@@ -621,6 +621,115 @@ __global__ __launch_bounds__(512) void k_vocab_small(GemmArgs a) {
   }
 }
 
+// ============================================================ vocabulary projection, one window
+// The single-window step's logits (<= 8 rows: one window's beams, fp16, K = 1280) with the
+// decoder's final LayerNorm in the prologue, as k_vocab_small, but balanced over the chip:
+// k_vocab_small gives every WAVE whole 16-column tiles over all of K, and 3242 tiles over
+// 2048 waves leave 1194 waves with two tiles and 854 with one (the launch lasts two
+// tiles: 133 MB at ~4 TB/s).  Here workgroup b owns the contiguous tiles
+// [b nt / 256, (b + 1) nt / 256) (12 or 13: every CU streams 520 KB +- 4 %), and its 8 waves
+// split K into eighths (5 k-steps each) across ALL of those tiles; the 8 partial tiles are
+// summed in LDS in wave order (fixed: deterministic).  The tile loop is unrolled to its
+// TMAX = 13 tiles and its weight fragments stream through a ring of D tiles: tile t + D - 1
+// is issued while tile t is multiplied, so a wave keeps D x 5 KB in flight from its first
+// instruction to its last (a workgroup of 12 tiles re-reads its last tile as the 13th and
+// stores nothing for it).  The LayerNorm operands are issued BEFORE the first weight
+// fragments, so normalising waits only for them.  Per row the k order is: the wave's 5
+// k-steps ascending, the 8 eighths in order — its own fixed order (this kernel serves only
+// n_win == 1 batches, whose step is already its own path: DESIGN.md §2).
+template <int D>
+__global__ __launch_bounds__(512) void k_vocab1(GemmArgs a) {
+  constexpr int KW = 8, SW = 5, K = KW * SW * 32, TMAX = 13;  // K 1280, <= 13 tiles (launcher)
+  constexpr int XROW = K * 2 + 16;
+  extern __shared__ __attribute__((aligned(16))) char xs1[];
+  float4_t* red = reinterpret_cast<float4_t*>(xs1 + 8 * XROW);  // [TMAX tiles][KW][64]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = lane & 15, g = lane >> 4;
+  const int nt = (a.N + 15) / 16, b = blockIdx.x, nb = gridDim.x;
+  const int t0 = (int)((int64_t)b * nt / nb), t1 = (int)((int64_t)(b + 1) * nt / nb), ntl = t1 - t0;
+  const half_t* W = reinterpret_cast<const half_t*>(a.W);
+  const int kb = wave * SW * 32;
+  auto load_tile = [&](int tl, Frag<half_t> (&wf)[SW]) {
+    const int tile = t0 + min(tl, ntl - 1);
+    const half_t* wp = W + (int64_t)min(tile * 16 + r, a.N - 1) * K + kb + 8 * g;
+#pragma unroll
+    for (int s = 0; s < SW; ++s) frag_load_stream(wf[s], wp + s * 32);
+  };
+  // the final LayerNorm of the fp32 residual rows (k_vocab_small's prologue): one wave per
+  // row; its operands go out first
+  constexpr int CPLM = 5;
+  const int row = wave;
+  const bool lnrow = row < a.M;
+  float4_t xv[CPLM], gv[CPLM], bv[CPLM];
+  if (lnrow) {
+    const float* xr = a.xf32 + (int64_t)row * K;
+#pragma unroll
+    for (int i = 0; i < CPLM; ++i) {
+      const int c = lane + 64 * i;
+      xv[i] = load4f(xr + 4 * c);
+      gv[i] = load4f(a.ln_g + 4 * c);
+      bv[i] = load4f(a.ln_b + 4 * c);
+    }
+  }
+  Frag<half_t> wf[D][SW];
+#pragma unroll
+  for (int t = 0; t < D - 1; ++t) load_tile(t, wf[t]);
+  {
+    half_t* dst = reinterpret_cast<half_t*>(xs1 + row * XROW);
+    if (!lnrow) {
+      for (int c = lane; c < K / 4; c += 64) store4(dst + 4 * c, 0.f, 0.f, 0.f, 0.f);
+    } else {
+      float sm = 0.f;
+#pragma unroll
+      for (int i = 0; i < CPLM; ++i) sm += xv[i][0] + xv[i][1] + xv[i][2] + xv[i][3];
+      const float mean = wave_sum(sm) / (float)K;
+      float q = 0.f;
+#pragma unroll
+      for (int i = 0; i < CPLM; ++i)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float d = xv[i][e] - mean;
+          q += d * d;
+        }
+      const float rstd = rsqrtf(wave_sum(q) / (float)K + a.ln_eps);
+#pragma unroll
+      for (int i = 0; i < CPLM; ++i) {
+        const float4_t v = xv[i];
+        store4(dst + 4 * (lane + 64 * i), (v[0] - mean) * rstd * gv[i][0] + bv[i][0],
+               (v[1] - mean) * rstd * gv[i][1] + bv[i][1], (v[2] - mean) * rstd * gv[i][2] + bv[i][2],
+               (v[3] - mean) * rstd * gv[i][3] + bv[i][3]);
+      }
+    }
+  }
+  __syncthreads();
+  // this wave's X fragments (rows r < 8 valid; rows 8..15 repeat row 7, never stored)
+  Frag<half_t> xf[SW];
+#pragma unroll
+  for (int s = 0; s < SW; ++s)
+    frag_load(xf[s], reinterpret_cast<const half_t*>(xs1 + min(r, 7) * XROW) + kb + s * 32 + 8 * g);
+#pragma unroll
+  for (int t = 0; t < TMAX; ++t) {
+    if (t + D - 1 < TMAX) load_tile(t + D - 1, wf[(t + D - 1) % D]);
+    float4_t acc = (float4_t){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < SW; ++s) mfma_step(acc, wf[t % D][s], xf[s]);
+    if (t < ntl) red[(t * KW + wave) * 64 + lane] = acc;
+  }
+  __syncthreads();
+  // per tile: the 8 eighths in wave order; lane (r, g) of a tile: row r, columns 4g .. +3
+  const auto rs = wt_rsrc(a.out_f32);
+  for (int i = tid; i < ntl * 64; i += 512) {
+    const int tl = i >> 6, ln = i & 63, rr = ln & 15, n = (t0 + tl) * 16 + 4 * (ln >> 4);
+    float4_t v = red[(tl * KW) * 64 + ln];
+#pragma unroll
+    for (int w = 1; w < KW; ++w) v += red[(tl * KW + w) * 64 + ln];
+    if (rr < a.M) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        if (n + e < a.N) wt_store1(rs, (rr * a.ldo + n + e) * 4, v[e]);
+    }
+  }
+}
+
 // ============================================================ vocabulary projection, 33-112 rows
 // The decoder step's logits for a whole batch (20 windows x 5 beams = 100 rows) against
 // the token embedding (133 MB fp16): every row is resident in LDS, HALF of K at a time
@@ -911,7 +1020,22 @@ int launch_gemm_tiles(const GemmArgs& a, int epi, int tile_sel, hipStream_t st) 
     }();
     if (a.xf32 && !(vocab_small && epi == EPI_F32_COLS && a.N >= 16384 && a.M <= 8 && a.K <= 1280 && a.K % 32 == 0 &&
                     !a.x_rows))
-      return -6;  // the LayerNorm prologue exists only in k_vocab_small
+      return -6;  // the LayerNorm prologue exists only in k_vocab_small / k_vocab1
+    // the single-window step (LayerNorm prologue, fp16, K 1280): k_vocab1, balanced over the
+    // chip (WHISPER_HIP_VOCAB1=0 in the tuning build: k_vocab_small)
+    static const bool vocab1 = [] {
+      const char* e = tune_env("WHISPER_HIP_VOCAB1");
+      return !(e && e[0] == '0');
+    }();
+    if (sizeof(T) == 2 && vocab1 && a.xf32 && a.K == 1280 && !a.bias && a.M <= 8 && (a.N + 15) / 16 <= 256 * 13) {
+      constexpr int D = 6;  // (N + 15) / 16 <= 256 x 13: at most 13 tiles per workgroup (TMAX)
+      const int lds = 8 * (1280 * 2 + 16) + 13 * 8 * 64 * 16;
+      static bool attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_vocab1<D>),
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) == hipSuccess;
+      if (!attr) return -5;
+      k_vocab1<D><<<256, 512, lds, st>>>(a);
+      return 0;
+    }
     // k_vocab_small: the rows in groups of <= 64 that fit LDS with all of K (152 KB)
     const int vxrow = a.K * (int)sizeof(T) + 16;
     const int vrg_max = std::min(64, (152 * 1024) / vxrow);

@@ -10,9 +10,12 @@ constexpr int TKP = 1536;  // cross-KV keys per (window, head) block: 1500 padde
 template <typename T>
 void launch_layernorm(const float* x, T* y, const float* g, const float* b, int rows, int n, float eps,
                       const int* rows_in, hipStream_t st);
+// Split-K slabs of the decoder-step projections (k_proj EPI_PARTIAL) are fp32, or fp16 in
+// fp16 contexts (GemmArgs::slab_half): `part` then points at half_t
+// elements and slab_half is 1.  Strides count elements.
 template <typename T>
 void launch_resid_ln(float* x, const float* part, int nsplit, int64_t part_stride, const float* bias, T* y,
-                     const float* g, const float* b, int rows, int n, float eps, hipStream_t st);
+                     const float* g, const float* b, int rows, int n, float eps, hipStream_t st, int slab_half = 0);
 template <typename T>
 void launch_attn_enc(const T* qkv, int ld, int ns, int H, int Tlen, int nwin, int64_t wsi, const T* vt, int tkp, T* out,
                      int64_t wso, hipStream_t st);
@@ -23,15 +26,16 @@ void launch_self_attn(const T* q, int ldq, const T* kc, const T* vc, const int* 
 template <typename T>
 int launch_self_attn_qkv(const float* part, int nsplit, int64_t part_stride, const float* bqkv, int ns, T* kc, T* vc,
                           const int* rw, const int* rs, const int* rp, const int* anc, int anc_beams, int nbeam, int H,
-                          int ctx, T* out, int ldo, int rows, hipStream_t st);
+                          int ctx, T* out, int ldo, int rows, hipStream_t st, int slab_half = 0);
 template <typename T>
 void launch_reduce_store(const float* part, int nsplit, int64_t part_stride, const float* bias, T* out, int ldo, int M,
-                         int N, int gelu, hipStream_t st);
+                         int N, int gelu, hipStream_t st, int slab_half = 0);
 // decoder-step query given as split-K slabs: q = bias + sum_z part[z*stride + row*ldq + c]
 // (part == nullptr: q is a T matrix); needs <= 16 rows per window and z in {4, 8, 10}
 // (cross_attn_q_slabs(z)).
 struct XQPart {
-  const float* part = nullptr;
+  const float* part = nullptr;  // half_t elements when part_half
+  int part_half = 0;
   int64_t stride = 0;
   int z = 0;
   const float* bias = nullptr;
@@ -87,6 +91,7 @@ struct DecState {
   int* cand_idx;     // [nw*G][KC]
   float* lpart;      // [nw*G][LP_SLICES][LP_REC] per-slice token-selection partials
   int* lp_cnt;       // [nw*G] slice arrival counters of k_logit_part (zero between launches)
+  int* lpw_cnt;      // [nw] row arrival counters of the merging k_logit_part (zero between launches)
   unsigned long long* seed;  // [1] sampling seed (device memory: not part of a captured graph)
   int nw, G, ctx, hctx, maxc;
 };
@@ -106,7 +111,21 @@ struct DecOpts {
 constexpr int LP_SLICES = 32;  // vocabulary slices per row: 31 text slices + [timestamp_begin, V)
 constexpr int LP_REC = 32;    // words per slice record
 void launch_logit_rows(float* logits, int ldl, const DecState& s, const DecOpts& o, int nwin, hipStream_t st);
-void launch_merge(const DecState& s, const DecOpts& o, int nwin, hipStream_t st);
+// k_merge also writes the NEXT step's decoder input rows (the embedding of each row's
+// newest token, k_embed's arithmetic) when em.x is set: the step graph then starts with
+// the first layer instead of a separate k_embed launch (round 4)
+struct MergeEmbed {
+  const void* E = nullptr;  // token embedding [V][n] (T)
+  const void* P = nullptr;  // positional embedding [ctx][n] (T)
+  float* x = nullptr;       // decoder input rows [rows][n] (fp32)
+  int* row_pos = nullptr;   // position of each row's input token
+  int n = 0, pmax = 0, half = 0;
+};
+void launch_merge(const DecState& s, const DecOpts& o, int nwin, hipStream_t st, const MergeEmbed& em = MergeEmbed());
+// token selection + candidate merge of one update: one k_logit_part launch whose last
+// row combiner of each window runs the merge (round 4), or k_logit_* then k_merge
+void launch_select_merge(float* logits, int ldl, const DecState& s, const DecOpts& o, int nwin, hipStream_t st,
+                         const MergeEmbed& em);
 // per-step ABI (wh_step / wh_reorder_kv): append host-chosen tokens, reorder rows
 void launch_append_tokens(const DecState& s, const int* tok, int nwin, hipStream_t st);
 void launch_reorder_rows(const DecState& s, const int* src, int nwin, hipStream_t st);

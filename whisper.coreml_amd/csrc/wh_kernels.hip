@@ -1,6 +1,8 @@
 // Attention, LayerNorm, embedding and log-mel kernels for libwhisper_hip.
 #include "wh_kernels.h"
 
+#include <cstdio>
+#include <type_traits>
 #include <cstdlib>
 
 namespace wh {
@@ -65,8 +67,8 @@ void launch_layernorm(const float* x, T* y, const float* g, const float* b, int 
 // x[r] += bias + sum_s part[s][r] (fixed order: deterministic split-K reduction of the
 // residual GEMVs), then y = LayerNorm(x).  One 256-thread block per row; every load
 // of the row is issued before the first reduction (latency-bound at decode sizes).
-template <typename T, int NS, int MAXV = 2>
-__global__ __launch_bounds__(512) void k_resid_ln(float* __restrict__ x, const float* __restrict__ part, int nsplit,
+template <typename T, int NS, int MAXV = 2, typename S = float>
+__global__ __launch_bounds__(512) void k_resid_ln(float* __restrict__ x, const S* __restrict__ part, int nsplit,
                                                   int64_t part_stride, const float* __restrict__ bias,
                                                   T* __restrict__ y, const float* __restrict__ gamma,
                                                   const float* __restrict__ beta, int n, float eps) {
@@ -84,14 +86,17 @@ __global__ __launch_bounds__(512) void k_resid_ln(float* __restrict__ x, const f
       gm[i] = load4f(gamma + 4 * c);
       bt[i] = load4f(beta + 4 * c);
       float4_t a = load4f(xr + 4 * c);
-      float4_t pp[NS > 0 ? NS : 1];
+      // the slabs' raw elements first, converted after every load is issued (an fp16 slab
+      // converted where it is loaded puts a wait behind each predicated load)
+      typedef typename std::conditional<sizeof(S) == 2, half4_t, float4_t>::type R4;
+      R4 pp[NS > 0 ? NS : 1];
 #pragma unroll
       for (int sp = 0; sp < NS; ++sp)
-        if (sp < nsplit) pp[sp] = load4f(part + sp * part_stride + (int64_t)row * n + 4 * c);
+        if (sp < nsplit) pp[sp] = *reinterpret_cast<const R4*>(part + sp * part_stride + (int64_t)row * n + 4 * c);
       if (bias) a += load4f(bias + 4 * c);
 #pragma unroll
       for (int sp = 0; sp < NS; ++sp)
-        if (sp < nsplit) a += pp[sp];
+        if (sp < nsplit) a += (float4_t){(float)pp[sp][0], (float)pp[sp][1], (float)pp[sp][2], (float)pp[sp][3]};
       v[i] = a;
     }
   }
@@ -136,12 +141,18 @@ __global__ __launch_bounds__(512) void k_resid_ln(float* __restrict__ x, const f
 
 template <typename T>
 void launch_resid_ln(float* x, const float* part, int nsplit, int64_t part_stride, const float* bias, T* y,
-                     const float* g, const float* b, int rows, int n, float eps, hipStream_t st) {
+                     const float* g, const float* b, int rows, int n, float eps, hipStream_t st, int slab_half) {
   if (rows <= 0) return;
   // one float4 per thread (n <= 2048; 1280: 5 waves); tuning builds WHISPER_HIP_RLN_256=1
   // for the round-3 form (256 threads, up to two float4 each)
   const char* e = tune_env("WHISPER_HIP_RLN_256");
   const int nt = (e && atoi(e) == 1) ? 256 : ((n >> 2) + 63) / 64 * 64;
+  if (slab_half && nsplit > 0 && nt != 256) {  // fp16 slabs (fp16 contexts, k_proj)
+    const half_t* ph = reinterpret_cast<const half_t*>(part);
+    if (nsplit <= 4) k_resid_ln<T, 4, 1, half_t><<<rows, nt, 0, st>>>(x, ph, nsplit, part_stride, bias, y, g, b, n, eps);
+    else k_resid_ln<T, 16, 1, half_t><<<rows, nt, 0, st>>>(x, ph, nsplit, part_stride, bias, y, g, b, n, eps);
+    return;
+  }
 #define RLN(NS_, MV_) \
   k_resid_ln<T, NS_, MV_><<<rows, nt, 0, st>>>(x, part, NS_ ? nsplit : 0, part_stride, bias, y, g, b, n, eps)
   if (nsplit <= 0) {
@@ -736,10 +747,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void
 template <typename T>
 int launch_self_attn_qkv(const float* part, int nsplit, int64_t part_stride, const float* bqkv, int ns, T* kc, T* vc,
                           const int* rw, const int* rs, const int* rp, const int* anc, int anc_beams, int nbeam, int H,
-                          int ctx, T* out, int ldo, int rows, hipStream_t st) {
+                          int ctx, T* out, int ldo, int rows, hipStream_t st, int slab_half) {
   if (rows <= 0) return 0;
   // the kernel takes window and beam from the row index: step rows are w * G + beam
-  if (anc_beams < 1 || rows % anc_beams) return -1;
+  // fp32 slabs only: the (row, head) wave reads its q / k / v columns lane per element
+  // (an fp16-slab form measured 8.7 -> 13.9 us per launch)
+  if (anc_beams < 1 || rows % anc_beams || nsplit > 16 || slab_half) return -1;
   k_self_attn_qkv<T><<<rows * H, 64, 0, st>>>(part, nsplit, part_stride, bqkv, ns, kc, vc, rw, rs, rp, anc, anc_beams,
                                              nbeam, H, ctx, out, ldo);
   return 0;
@@ -747,21 +760,22 @@ int launch_self_attn_qkv(const float* part, int nsplit, int64_t part_stride, con
 
 // out[m][n] = act(bias[n] + sum_z part[z][m][n]) as T (split-K epilogue of the
 // non-residual decoder GEMVs: cross-attention query, MLP fc1 + GELU)
-template <typename T, int ACT>
-__global__ __launch_bounds__(256) void k_reduce_store(const float* __restrict__ part, int nsplit, int64_t part_stride,
+template <typename T, int ACT, typename S = float>
+__global__ __launch_bounds__(256) void k_reduce_store(const S* __restrict__ part, int nsplit, int64_t part_stride,
                                                       const float* __restrict__ bias, T* __restrict__ out, int ldo, int M,
                                                       int N) {
   const int64_t i = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4;
   if (i >= (int64_t)M * N) return;
   const int m = (int)(i / N), n = (int)(i - (int64_t)m * N);
-  float4_t pp[16];
+  typedef typename std::conditional<sizeof(S) == 2, half4_t, float4_t>::type R4;  // raw slab elements
+  R4 pp[16];
 #pragma unroll
   for (int z = 0; z < 16; ++z)
-    if (z < nsplit) pp[z] = load4f(part + z * part_stride + i);
+    if (z < nsplit) pp[z] = *reinterpret_cast<const R4*>(part + z * part_stride + i);
   float4_t v = bias ? load4f(bias + n) : (float4_t){0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int z = 0; z < 16; ++z)
-    if (z < nsplit) v += pp[z];
+    if (z < nsplit) v += (float4_t){(float)pp[z][0], (float)pp[z][1], (float)pp[z][2], (float)pp[z][3]};
   if (ACT) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) v[j] = gelu_f(v[j]);
@@ -771,10 +785,16 @@ __global__ __launch_bounds__(256) void k_reduce_store(const float* __restrict__ 
 
 template <typename T>
 void launch_reduce_store(const float* part, int nsplit, int64_t part_stride, const float* bias, T* out, int ldo, int M,
-                         int N, int gelu, hipStream_t st) {
+                         int N, int gelu, hipStream_t st, int slab_half) {
   if (M <= 0) return;
   const int64_t tot = (int64_t)M * N / 4;
   const unsigned nb = (unsigned)((tot + 255) / 256);
+  if (slab_half) {
+    const half_t* ph = reinterpret_cast<const half_t*>(part);
+    if (gelu) k_reduce_store<T, 1, half_t><<<nb, 256, 0, st>>>(ph, nsplit, part_stride, bias, out, ldo, M, N);
+    else k_reduce_store<T, 0, half_t><<<nb, 256, 0, st>>>(ph, nsplit, part_stride, bias, out, ldo, M, N);
+    return;
+  }
   if (gelu) k_reduce_store<T, 1><<<nb, 256, 0, st>>>(part, nsplit, part_stride, bias, out, ldo, M, N);
   else k_reduce_store<T, 0><<<nb, 256, 0, st>>>(part, nsplit, part_stride, bias, out, ldo, M, N);
 }
@@ -1024,7 +1044,7 @@ WH_DEV float4_t xs_merge(int n, Get get) {
   return acc * inv;
 }
 
-template <typename T, int QZ, int RR>
+template <typename T, int QZ, int RR, typename S = float>
 __global__ __launch_bounds__(512, 1) void k_xattn_seg(const T* __restrict__ q, int ldq, const T* ck, const T* cvt, int Tk,
                                                      int H, int npair, int nsp, const int* __restrict__ win_row0,
                                                      const int* __restrict__ win_nrows,
@@ -1126,7 +1146,7 @@ __global__ __launch_bounds__(512, 1) void k_xattn_seg(const T* __restrict__ q, i
     float4_t qv = (float4_t){0.f, 0.f, 0.f, 0.f};
     if constexpr (QP) {
       float4_t pp[QP ? QZ : 1];
-      const float* src = xq.part + (int64_t)row * ldq + c;
+      const S* src = reinterpret_cast<const S*>(xq.part) + (int64_t)row * ldq + c;
 #pragma unroll
       for (int z = 0; z < QZ; ++z) pp[z] = load4f(src + z * xq.stride);
       qv = load4f(xq.bias + c);
@@ -1261,11 +1281,18 @@ void launch_cross_attn(const T* q, int ldq, const T* ck, const T* cv, int Tk, in
       nwin * H <= xq.max_pairs) {
     const int npair = nwin * H;
 #define XS(QZ_, RR_)                                                                                              \
-  k_xattn_seg<T, QZ_, RR_><<<xattn_seg_grid(npair, nsp, XsShape<RR_>::SMAX), 512, 0, st>>>(                  \
-      q, ldq, ck, cv, Tk, H, npair, nsp, win_row0, win_nrows, win_slot, win_stride, xq, out, ldo)
+  if (xq.part_half)                                                                                             \
+    k_xattn_seg<T, QZ_, RR_, half_t><<<xattn_seg_grid(npair, nsp, XsShape<RR_>::SMAX), 512, 0, st>>>(          \
+        q, ldq, ck, cv, Tk, H, npair, nsp, win_row0, win_nrows, win_slot, win_stride, xq, out, ldo);              \
+  else                                                                                                          \
+    k_xattn_seg<T, QZ_, RR_><<<xattn_seg_grid(npair, nsp, XsShape<RR_>::SMAX), 512, 0, st>>>(                  \
+        q, ldq, ck, cv, Tk, H, npair, nsp, win_row0, win_nrows, win_slot, win_stride, xq, out, ldo)
 #define XSR(QZ_)                        \
-  if (xq.max_rows <= 8) XS(QZ_, 8);     \
-  else XS(QZ_, 16);
+  if (xq.max_rows <= 8) {               \
+    XS(QZ_, 8);                         \
+  } else {                              \
+    XS(QZ_, 16);                        \
+  }
     switch (xq.part ? xq.z : 0) {
       case 4: XSR(4) break;
       case 8: XSR(8) break;
@@ -1277,7 +1304,12 @@ void launch_cross_attn(const T* q, int ldq, const T* ck, const T* cv, int Tk, in
     return;
   }
   // first passes (prefill, alignment capture): one 64-key tile per wave, 8 waves per
-  // split, partials combined by k_cross_combine
+  // split, partials combined by k_cross_combine (fp32 query slabs only: the runtime hands
+  // fp16 slabs to the step kernel above alone)
+  if (xq.part_half) {
+    fprintf(stderr, "launch_cross_attn: fp16 query slabs outside the step kernel\n");
+    abort();
+  }
   constexpr int NW = 8;
   nsplit = (nsp + NW - 1) / NW;
   const dim3 grid(nwin, H, nsplit);
@@ -1462,10 +1494,11 @@ void launch_mel_norm(float* mel, int64_t count, int64_t ld, int n_mels, const un
   template void launch_layernorm<T>(const float*, T*, const float*, const float*, int, int, float, const int*,     \
                                     hipStream_t);                                                                   \
   template void launch_resid_ln<T>(float*, const float*, int, int64_t, const float*, T*, const float*, const float*, \
-                                   int, int, float, hipStream_t);                                                   \
+                                   int, int, float, hipStream_t, int);                                              \
   template int launch_self_attn_qkv<T>(const float*, int, int64_t, const float*, int, T*, T*, const int*, const int*, \
-                                        const int*, const int*, int, int, int, int, T*, int, int, hipStream_t);     \
-  template void launch_reduce_store<T>(const float*, int, int64_t, const float*, T*, int, int, int, int, hipStream_t); \
+                                        const int*, const int*, int, int, int, int, T*, int, int, hipStream_t, int); \
+  template void launch_reduce_store<T>(const float*, int, int64_t, const float*, T*, int, int, int, int, hipStream_t, \
+                                       int);                                                                        \
   template void launch_attn_enc<T>(const T*, int, int, int, int, int, int64_t, const T*, int, T*, int64_t,         \
                                    hipStream_t);                                                                    \
   template void launch_self_attn<T>(const T*, int, const T*, const T*, const int*, const int*, const int*,         \

@@ -135,8 +135,18 @@ __global__ __launch_bounds__(64 * NSUB * KW) void k_proj(GemmArgs a) {
     float4_t v = acc[mt];
     if constexpr (EPI == EPI_PARTIAL) {
 #if WH_WT
-      // write-through (sc1): the slab leaves no dirty L2 lines for the kernel-end release
-      wt_store4(wt_rsrc(a.out_f32), (int)((((int64_t)kz * a.M + m) * a.ldo + n) * 4), v);
+      // write-through (sc1): the slab leaves no dirty L2 lines for the kernel-end release;
+      // fp16 contexts store fp16 slabs (8 B per lane): half the bytes written here and read
+      // by every consumer (round 4: out seam 9.50 -> 8.37 us in a graph chain,
+      // profiles/r04/fp16_slab_chain_bench.txt)
+      const int64_t e = ((int64_t)kz * a.M + m) * a.ldo + n;
+      if (sizeof(T) == 2 && a.slab_half) {
+        typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+        const half4_t hv = (half4_t){(half_t)v[0], (half_t)v[1], (half_t)v[2], (half_t)v[3]};
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, hv), wt_rsrc(a.out_f32), (int)(e * 2), 0, 16);
+      } else {
+        wt_store4(wt_rsrc(a.out_f32), (int)(e * 4), v);
+      }
 #else
       store4(a.out_f32 + ((int64_t)kz * a.M + m) * a.ldo + n, v[0], v[1], v[2], v[3]);
 #endif

@@ -128,6 +128,9 @@ struct wh_ctx {
                           int* plens) = 0;
   virtual int dtw(const float* x, int N, int M, int* path, int* plen) = 0;
   virtual int time_stage(int what, int iters, double* ms) = 0;
+  // tuning builds only (wh_tune_share_weights): read the weights of another context of the
+  // same dims and dtype instead of this one's (probes of two window groups, one weight copy)
+  virtual int share_weights_from(wh_ctx* src) = 0;
   std::vector<float> token_ms;  // per-token wall ms of each decode_steps chunk
   double stats[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   int maxc = 5;
@@ -215,6 +218,19 @@ struct Ctx : public wh_ctx {
   Timer tm;
   std::vector<hipEvent_t> proj_ev;  // time_stage(7) event pairs, empty otherwise
   int proj_ev_n = 0;
+
+  int share_weights_from(wh_ctx* src_) override {
+    auto* src = dynamic_cast<Ctx<T>*>(src_);
+    if (!src || src->ns != ns || src->Ld != Ld || src->La != La || src->V != V || !src->finalized)
+      return fail(-2, "share_weights: a finalized context of the same dims and dtype is needed");
+    conv1_w = src->conv1_w; conv2_w = src->conv2_w; E = src->E; Pdec = src->Pdec; ckv_w = src->ckv_w;
+    conv1_b = src->conv1_b; conv2_b = src->conv2_b; pos_enc = src->pos_enc; lnp_g = src->lnp_g; lnp_b = src->lnp_b;
+    ln_g = src->ln_g; ln_b = src->ln_b; ckv_b = src->ckv_b;
+    enc = src->enc;
+    dec = src->dec;
+    finalized = true;
+    return 0;
+  }
 
   ~Ctx() override {
     if (gexec) hipGraphExecDestroy(gexec);
@@ -329,6 +345,7 @@ struct Ctx : public wh_ctx {
     addA(Wcap * 16 * 4); addA(Wcap * 16 * 4); addA((size_t)Wcap * 16 * HCTX * 4);
     addA((size_t)Wcap * Gcap * KC * 4); addA((size_t)Wcap * Gcap * KC * 4);
     addA((size_t)Wcap * Gcap * LP_SLICES * LP_REC * 4); addA((size_t)Wcap * Gcap * 4);
+    addA((size_t)Wcap * 4);  // window arrival counters of the merging selection
     addA(64);
     addA(64);
     addA((size_t)P1_SLABS * 256 * 4); addA((size_t)(4 * n / 16) * 4);  // k_proj1 split-K slabs + counters
@@ -365,11 +382,12 @@ struct Ctx : public wh_ctx {
     S.fin_score = fa(Wcap * 16); S.fin_len = ia(Wcap * 16); S.fin_tok = ia((size_t)Wcap * 16 * HCTX);
     S.cand_val = fa((size_t)Wcap * Gcap * KC); S.cand_idx = ia((size_t)Wcap * Gcap * KC);
     S.lpart = fa((size_t)Wcap * Gcap * LP_SLICES * LP_REC); S.lp_cnt = ia((size_t)Wcap * Gcap);  // zeroed with the arena
+    S.lpw_cnt = ia((size_t)Wcap);
     S.seed = (unsigned long long*)aa.take(64);
     p1_slab = fa((size_t)P1_SLABS * 256); p1_cnt = ia(4 * n / 16);  // zeroed with the arena
     xs_rec = fa((size_t)Wcap * nh * XS_NSP * XREC); xs_cnt = ia((size_t)Wcap * nh);
     x2_d = fa((size_t)8 * n);
-    if (!S.seed || !S.cand_idx || !S.lp_cnt || !p1_cnt || !xs_cnt || !x2_d) return fail(-3, "activation arena overflow");
+    if (!S.seed || !S.cand_idx || !S.lp_cnt || !S.lpw_cnt || !p1_cnt || !xs_cnt || !x2_d) return fail(-3, "activation arena overflow");
     S.nw = Wcap; S.G = 1; S.ctx = CTX; S.hctx = HCTX; S.maxc = 16;
     HIPCHK(hipMalloc(&d_gmax, 64));
     d_gmax_f = (float*)(d_gmax + 4);
@@ -717,10 +735,23 @@ struct Ctx : public wh_ctx {
 
   // X[R][K] W^T into the split-K partial slabs part[z][R][N]: k_proj where a tile
   // configuration fits (decode rows <= 112), the k_gemv path otherwise; *ks = z
-  int partial(const void* X, int ldx, const T* W, int R, int N, int K, int* ks) {
+  // Slabs are fp32.  WHISPER_HIP_SLAB16=1 (tuning build only) has k_proj store them as fp16
+  // (slab_h = 1 after such a partial()): at 20 windows it cut the step's summed kernel time
+  // by 0.3 % (profiles/r04/slab16_ab.txt), not worth fp16-rounded partial sums.
+  int slab_h = 0;
+  static bool slab16_enabled() {
+    static const bool on = [] {
+      const char* e = tune_env("WHISPER_HIP_SLAB16");
+      return e && e[0] == '1';
+    }();
+    return on;
+  }
+  int partial(const void* X, int ldx, const T* W, int R, int N, int K, int* ks, bool half_ok = true) {
     GemmArgs g;
     g.X = X; g.ldx = ldx; g.W = W; g.M = R; g.N = N; g.K = K; g.x_group_rows = R;
     g.out_f32 = part; g.ldo = N;
+    g.slab_half = half_ok && sizeof(T) == 2 && slab16_enabled();
+    slab_h = g.slab_half;
     const int maxz = part_slabs(R, N);
     // time_stage(7): each k_proj of an eager step timed by its own dispatch events
     const bool tev = proj_ev_n < (int)proj_ev.size() / 2;
@@ -729,6 +760,7 @@ struct Ctx : public wh_ctx {
     if (tev && rc == 0) ++proj_ev_n;
     if (rc == 0) return 0;
     if (rc != -1) return fail(-20, "k_proj launch failed code " + std::to_string(rc));
+    slab_h = 0;
     *ks = gemv_ksplit(R, N, K, maxz);
     g = GemmArgs();
     g.out_f32 = part; g.ldo = N; g.ksplit = *ks;
@@ -745,7 +777,7 @@ struct Ctx : public wh_ctx {
     } else {
       int ks = 0;
       TRY(partial(X, K, W, R, n, K, &ks));
-      launch_resid_ln<T>(x_d, part, ks, (int64_t)R * n, b, xn_d, lg, lb, R, n, 1e-5f, st);
+      launch_resid_ln<T>(x_d, part, ks, (int64_t)R * n, b, xn_d, lg, lb, R, n, 1e-5f, st, slab_h);
     }
     return 0;
   }
@@ -757,7 +789,7 @@ struct Ctx : public wh_ctx {
     if (skinny) {
       int ks = 0;
       TRY(partial(xn_d, ns, W, R, N, ns, &ks));
-      launch_reduce_store<T>(part, ks, (int64_t)R * N, b, out, N, R, N, gelu, st);
+      launch_reduce_store<T>(part, ks, (int64_t)R * N, b, out, N, R, N, gelu, st, slab_h);
     } else {
       g.out = out; g.ldo = N;
       TRY(gemm(xn_d, ns, W, b, R, N, ns, gelu ? EPI_STORE_GELU : EPI_STORE, g));
@@ -784,9 +816,9 @@ struct Ctx : public wh_ctx {
       auto& e = dec[l];
       if (skinny) {
         int ks = 0;
-        TRY(partial(xn_d, n, e.wqkv, R, 3 * n, n, &ks));
+        TRY(partial(xn_d, n, e.wqkv, R, 3 * n, n, &ks, false));  // k_self_attn_qkv reads fp32 slabs
         if (launch_self_attn_qkv<T>(part, ks, (int64_t)R * 3 * n, e.bqkv, n, kc[l], vc[l], rw, rs, rp, S.anc, ancG,
-                                    Gcap, nh, CTX, att_d, n, R, st))
+                                    Gcap, nh, CTX, att_d, n, R, st, slab_h))
           return fail(-20, "self-attention rows are not a whole number of beam groups");
       } else {
         g = GemmArgs();
@@ -804,9 +836,9 @@ struct Ctx : public wh_ctx {
         int ks = 0;
         TRY(partial(xn_d, n, e.wqx, R, n, n, &ks));
         if (cross_attn_q_slabs(ks)) {
-          xq.part = part; xq.stride = (int64_t)R * n; xq.z = ks; xq.bias = e.bqx;
+          xq.part = part; xq.part_half = slab_h; xq.stride = (int64_t)R * n; xq.z = ks; xq.bias = e.bqx;
         } else {
-          launch_reduce_store<T>(part, ks, (int64_t)R * n, e.bqx, q_d, n, R, n, 0, st);
+          launch_reduce_store<T>(part, ks, (int64_t)R * n, e.bqx, q_d, n, R, n, 0, st, slab_h);
         }
       } else {
         TRY(proj(e.wqx, e.bqx, R, n, q_d, 0, skinny));
@@ -1149,9 +1181,9 @@ struct Ctx : public wh_ctx {
     S.maxc = std::max(maxc, 1);
     maxc_stride = S.maxc;
     step_api = false;
-    // first update on the prefill logits (decoding.py:713-733, i == 0)
-    launch_logit_rows(logits, V, S, O, n_win, st);
-    launch_merge(S, O, n_win, st);
+    // first update on the prefill logits (decoding.py:713-733, i == 0); the merge also
+    // embeds each row's new token: the first step's input rows
+    launch_select_merge(logits, V, S, O, n_win, st, merge_embed());
     hipEventRecord(tm.b, st);
     HIPCHK(hipStreamSynchronize(st));
     HIPCHK(hipGetLastError());
@@ -1161,15 +1193,20 @@ struct Ctx : public wh_ctx {
     return 0;
   }
 
-  // one decoder step for the current batch (graph body)
+  // k_merge writes the next step's input rows (x_d, row_pos): no k_embed launch per token
+  MergeEmbed merge_embed() const {
+    MergeEmbed em;
+    em.E = E; em.P = Pdec; em.x = x_d; em.row_pos = row_pos; em.n = ns; em.pmax = CTX - 1; em.half = sizeof(T) == 2;
+    return em;
+  }
+  // one decoder step for the current batch (graph body); its input rows were embedded by
+  // the previous update's k_merge (decode_begin's first update for the first step)
   int step_body() {
     const int R = cur_nwin * cur_G;
-    launch_embed<T>(E, Pdec, ns, nullptr, row_pos, S.hist, S.len, cur_G, HCTX, CTX - 1, x_d, R, st);
     TRY(dec_layers(R, st_row_win, st_row_slot, row_pos, cur_G, cur_nwin, st_win_row0, st_win_nrows, st_win_slot,
                    nullptr, nullptr, 0, true));
     TRY(vocab(nullptr, R, logits));
-    launch_logit_rows(logits, V, S, O, cur_nwin, st);
-    launch_merge(S, O, cur_nwin, st);
+    launch_select_merge(logits, V, S, O, cur_nwin, st, merge_embed());
     return 0;
   }
 
@@ -1828,5 +1865,11 @@ int wh_sync(wh_ctx* ctx) {
   return 0;
 }
 int wh_time_stage(wh_ctx* ctx, int what, int iters, double* ms) { CTXCALL(ctx->time_stage(what, iters, ms)); }
+#if WH_TUNING
+int wh_tune_share_weights(wh_ctx* ctx, wh_ctx* src) {
+  if (!src) return fail(-1, "null source context");
+  CTXCALL(ctx->share_weights_from(src));
+}
+#endif
 
 }  // extern "C"

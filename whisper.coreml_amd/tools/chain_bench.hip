@@ -388,10 +388,52 @@ __global__ __launch_bounds__(64 * NSUB) void k_projv(GemmArgs a) {
   for (int mt = 0; mt < MT; ++mt) {
     const int m = mt * 16 + r;
     if (m >= a.M) continue;
-    if constexpr (MODE & 2) store4(a.out_f32 + ((int64_t)kz * a.M + m) * a.ldo + n, acc[mt][0], acc[mt][1], acc[mt][2],
+    if constexpr (MODE & 4) {  // fp16 slabs, write-through (8 B per lane)
+      const half4_t h = (half4_t){(half_t)acc[mt][0], (half_t)acc[mt][1], (half_t)acc[mt][2], (half_t)acc[mt][3]};
+      __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(unsigned __attribute__((ext_vector_type(2))), h), wt_rsrc(a.out_f32),
+                                            (int)((((int64_t)kz * a.M + m) * a.ldo + n) * 2), 0, 16);
+    } else if constexpr (MODE & 2) store4(a.out_f32 + ((int64_t)kz * a.M + m) * a.ldo + n, acc[mt][0], acc[mt][1], acc[mt][2],
                                    acc[mt][3]);
     else wt_store4(wt_rsrc(a.out_f32), (int)((((int64_t)kz * a.M + m) * a.ldo + n) * 4), acc[mt]);
   }
+}
+
+// k_resid_ln (wh_kernels.hip) reading fp16 slabs: one float4 of the row per thread
+template <int NS>
+__global__ __launch_bounds__(512) void k_rln16(float* __restrict__ x, const half_t* __restrict__ part, int64_t pstride,
+                                               const float* __restrict__ bias, half_t* __restrict__ y,
+                                               const float* __restrict__ gamma, const float* __restrict__ beta, int n,
+                                               float eps) {
+  __shared__ float red[2][8];
+  const int row = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, nwv = blockDim.x >> 6;
+  float* xr = x + (int64_t)row * n;
+  const int c = tid;
+  const float4_t gm = load4f(gamma + 4 * c), bt = load4f(beta + 4 * c);
+  float4_t a = load4f(xr + 4 * c);
+  float4_t pp[NS];
+#pragma unroll
+  for (int sp = 0; sp < NS; ++sp) pp[sp] = load4f(part + sp * pstride + (int64_t)row * n + 4 * c);
+  a += load4f(bias + 4 * c);
+#pragma unroll
+  for (int sp = 0; sp < NS; ++sp) a += pp[sp];
+  store4(xr + 4 * c, a[0], a[1], a[2], a[3]);
+  float s = wave_sum(a[0] + a[1] + a[2] + a[3]);
+  if (lane == 0) red[0][wv] = s;
+  __syncthreads();
+  float tot = 0.f;
+  for (int k = 0; k < nwv; ++k) tot += red[0][k];
+  const float mean = tot / (float)n;
+  float q = 0.f;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) q += (a[j] - mean) * (a[j] - mean);
+  q = wave_sum(q);
+  if (lane == 0) red[1][wv] = q;
+  __syncthreads();
+  float qt = 0.f;
+  for (int k = 0; k < nwv; ++k) qt += red[1][k];
+  const float rstd = rsqrtf(qt / (float)n + eps);
+  store4(y + (int64_t)row * n + 4 * c, (a[0] - mean) * rstd * gm[0] + bt[0], (a[1] - mean) * rstd * gm[1] + bt[1],
+         (a[2] - mean) * rstd * gm[2] + bt[2], (a[3] - mean) * rstd * gm[3] + bt[3]);
 }
 
 __global__ __launch_bounds__(256) void k_ingest(const float4_t* __restrict__ h, const float4_t* __restrict__ s, int h16,
@@ -564,6 +606,33 @@ int main(int argc, char** argv) {
   var("variant: local copy (write-through)", &k_projv<7, 4, 5, 0>);
   var("variant: no epilogue store", &k_projv<7, 4, 5, 1>);
   var("variant: plain stores", &k_projv<7, 4, 5, 2>);
+  // fp16 split-K slabs (half the slab bytes) + a k_resid_ln reading them
+  {
+    using PF = ProjShape<half_t, 7, 5, 1, 10>;
+    CK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_projv<7, 5, 10, 0>), hipFuncAttributeMaxDynamicSharedMemorySize,
+                           PF::LDS));
+    CK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_projv<7, 5, 10, 4>), hipFuncAttributeMaxDynamicSharedMemorySize,
+                           PF::LDS));
+    CK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_projv<7, 4, 5, 4>), hipFuncAttributeMaxDynamicSharedMemorySize,
+                           PS::LDS));
+    half_t* part16 = reinterpret_cast<half_t*>(part);
+    time_chain("fp32 slabs: out projv + rln", [&](int i) {
+      hipLaunchKernelGGL((k_projv<7, 4, 5, 0>), dim3(160), dim3(256), PS::LDS, st, proj_args(i, n, n));
+      launch_resid_ln<half_t>(x, part, 8, (int64_t)M * n, bias, Y, g, b, M, n, 1e-5f, st);
+    });
+    time_chain("fp16 slabs: out projv + rln16", [&](int i) {
+      hipLaunchKernelGGL((k_projv<7, 4, 5, 4>), dim3(160), dim3(256), PS::LDS, st, proj_args(i, n, n));
+      hipLaunchKernelGGL((k_rln16<8>), dim3(M), dim3(320), 0, st, x, part16, (int64_t)M * n, bias, Y, g, b, n, 1e-5f);
+    });
+    time_chain("fp32 slabs: fc2 projv + rln", [&](int i) {
+      hipLaunchKernelGGL((k_projv<7, 5, 10, 0>), dim3(256), dim3(320), PF::LDS, st, proj_args(i, n, 4 * n));
+      launch_resid_ln<half_t>(x, part, 16, (int64_t)M * n, bias, Y, g, b, M, n, 1e-5f, st);
+    });
+    time_chain("fp16 slabs: fc2 projv + rln16", [&](int i) {
+      hipLaunchKernelGGL((k_projv<7, 5, 10, 4>), dim3(256), dim3(320), PF::LDS, st, proj_args(i, n, 4 * n));
+      hipLaunchKernelGGL((k_rln16<16>), dim3(M), dim3(320), 0, st, x, part16, (int64_t)M * n, bias, Y, g, b, n, 1e-5f);
+    });
+  }
   // the same bytes per workgroup with nothing else: X slice 35 KB shared by 20, W 20 KB
   time_chain("ingest: 35 KB shared + 20 KB streamed", [&](int i) {
     k_ingest<<<160, 256, 0, st>>>(reinterpret_cast<const float4_t*>(W + wsz * (i % L)),
