@@ -13,6 +13,7 @@
 // k_merge     : one workgroup per window (candidate merge, history/ancestry update).
 #include <cstdlib>
 
+#include "wh_gemm.h"
 #include "wh_kernels.h"
 
 namespace wh {
@@ -341,6 +342,7 @@ __device__ void merge_embed(const MergeEmbed& em, int w, int G, int pos, const i
 
 template <int NT, bool SC1>
 __device__ __forceinline__ void merge_window(const DecState& s, const DecOpts& o, const MergeEmbed& em, int w, int tid, MergeLds& L) {
+  static_assert(NT >= MG_MAXG * KC, "one lane per candidate");
   const int G = s.G, len = s.len[w], sb = s.sample_begin[w];
   int* hist = s.hist + (int64_t)w * G * s.hctx;
   int* anc = s.anc + (int64_t)w * G * s.ctx;
@@ -391,26 +393,46 @@ __device__ __forceinline__ void merge_window(const DecState& s, const DecOpts& o
     }
     return;
   }
-  // stage old histories / ancestry
-  for (int i = tid; i < G * len; i += NT) {
-    const int b = i / len, p = i - b * len;
-    L.oh[b][p] = hist[b * s.hctx + p];
-    int a = (p < s.ctx) ? anc[b * s.ctx + p] : 0;
-    if (p == len - 1 && p >= sb) a = b;  // this step's KV of beam b was written in slot b
-    L.oa[b][p] = a;
-  }
-  // candidates in insertion order: beam-major, top-k order (decoding.py:366-373);
-  // at the first update all beams are identical: dict keys collapse onto beam 0's
-  // candidates with the source of the last duplicate (G-1).  Gathered by one lane
-  // each (independent loads), then ranked from LDS.
+  // stage old histories / ancestry and gather the candidates in ONE round trip: every
+  // load of the staging (unrolled, clamped addresses) and of the candidates is issued
+  // before the first LDS write.  Candidates in insertion order: beam-major, top-k order
+  // (decoding.py:366-373); at the first update all beams are identical: dict keys
+  // collapse onto beam 0's candidates with the source of the last duplicate (G-1).
   const bool first = (len == sb);
   const int nbeams = first ? 1 : G;
   const int nc = nbeams * (G + 1);
-  for (int c0 = tid; c0 < nc; c0 += NT) {
-    const int b = c0 / (G + 1), k = c0 - b * (G + 1), r = w * G + b;
-    L.csc[c0] = s.sum_lp[r] + cval(r * KC + k);
-    L.ctok[c0] = cidx(r * KC + k);
-    L.csrc[c0] = first ? (G - 1) : b;
+  constexpr int MU = (MG_MAXG * MG_MAXCTX + NT - 1) / NT;
+  const int nst = G * len;
+  int hv[MU], av[MU];
+#pragma unroll
+  for (int u = 0; u < MU; ++u) {
+    const int i = min(tid + NT * u, max(nst - 1, 0)), b = i / len, p = i - b * len;
+    hv[u] = hist[b * s.hctx + p];
+    av[u] = anc[b * s.ctx + min(p, s.ctx - 1)];
+  }
+  float cs = 0.f;
+  int ct = 0;
+  const bool cl = tid < nc;  // nc <= MG_MAXG * KC = 72 <= NT
+  if (cl) {
+    const int b = tid / (G + 1), k = tid - b * (G + 1), r = w * G + b;
+    cs = s.sum_lp[r] + cval(r * KC + k);
+    ct = cidx(r * KC + k);
+  }
+#pragma unroll
+  for (int u = 0; u < MU; ++u) {
+    const int i = tid + NT * u;
+    if (i < nst) {
+      const int b = i / len, p = i - b * len;
+      L.oh[b][p] = hv[u];
+      int a = (p < s.ctx) ? av[u] : 0;
+      if (p == len - 1 && p >= sb) a = b;  // this step's KV of beam b was written in slot b
+      L.oa[b][p] = a;
+    }
+  }
+  if (cl) {
+    L.csc[tid] = cs;
+    L.ctok[tid] = ct;
+    L.csrc[tid] = first ? (G - 1) : tid / (G + 1);
   }
   __syncthreads();
   // stable descending sort by rank (ties keep insertion order), then the walk of
@@ -980,6 +1002,492 @@ void launch_merge(const DecState& s, const DecOpts& o, int nwin, hipStream_t st,
 void launch_select_merge(float* logits, int ldl, const DecState& s, const DecOpts& o, int nwin, hipStream_t st,
                          const MergeEmbed& em) {
   if (!select_rows(logits, ldl, s, o, nwin, st, &em)) launch_merge(s, o, nwin, st, em);
+}
+
+// ------------------------------------------------------------ vocabulary + selection + merge, one window
+// The single-window step's whole token tail in ONE launch (round 4): k_vocab1's balanced
+// vocabulary projection (256 workgroups, 12-13 16-column tiles each, the final LayerNorm in
+// the prologue, a ring of D weight tiles in flight), then, per workgroup and row, the
+// selection of k_logit_part over the workgroup's own ~200 columns — filters, max, sum of
+// exp, top-(G+1) / argbest / Gumbel best — as a record per (row, part): part 0 the text
+// ids < timestamp_begin, part 1 the timestamp ids (only the workgroup straddling the
+// boundary has both), stored write-through.  The workgroup whose arrival completes the
+// launch merges every row's records (decoding.py:522-531: the timestamp-vs-text rule from
+// the combined normaliser and the two maxima; top-(G+1) across the records' sorted lists)
+// and then runs the window's candidate merge (merge_window) — no logits round trip, no
+// selection or merge launch.  Same choices as the sliced selection; the normaliser is
+// summed over other partitions, so log-probabilities can differ in the last bits.
+struct LpMasks {
+  int mlo[4], mhi[4], kid[5];
+};
+// the filters of decoding.py:450-532 for one row as four [lo, hi) masks and five ids
+__device__ __forceinline__ LpMasks lp_masks(const DecOpts& o, bool last_ts, bool penult_ts, bool first, int ts_last) {
+  const int tb = o.ts_begin, V = o.V;
+  LpMasks f;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) f.mlo[q] = f.mhi[q] = 0;
+#pragma unroll
+  for (int q = 0; q < 5; ++q) f.kid[q] = -1;
+  if (o.timestamps) {
+    if (last_ts) {
+      if (penult_ts) { f.mlo[0] = tb; f.mhi[0] = V; }
+      else { f.mlo[0] = 0; f.mhi[0] = o.eot; }
+    }
+    if (ts_last >= 0) {
+      f.mlo[1] = tb;
+      f.mhi[1] = (last_ts && !penult_ts) ? ts_last : ts_last + 1;
+    }
+    if (first) {
+      f.mlo[2] = 0; f.mhi[2] = tb;
+      if (o.max_initial >= 0) { f.mlo[3] = tb + o.max_initial + 1; f.mhi[3] = V; }
+    }
+    f.kid[4] = o.no_ts;
+  }
+  if (first && o.suppress_blank)
+#pragma unroll
+    for (int b = 0; b < 4; ++b)
+      if (b < o.n_blank) f.kid[b] = o.blank[b];
+  return f;
+}
+
+struct VsArgs {
+  DecState s;
+  DecOpts o;
+  MergeEmbed em;
+  float* rec;  // [VS_ROWS][2 parts][VS_NB workgroups][VS_REC]
+  int* cnt;    // the launch's arrival counter (zero between launches)
+};
+constexpr int VS_ROWS = 8, VS_NB = 256, VS_REC = 32, VS_TMAX = 13;
+// record words: 0 mx, 1 se, 2 bv, 3 bi, 4 gv, 5 gi, 6 gx, 8.. tv[KC], 8 + KC.. ti[KC]
+constexpr int VS_TV = 8, VS_TI = 8 + KC;
+static_assert(VS_TI + KC <= VS_REC, "record size");
+
+#if WH_TUNING
+// tuning build: per-workgroup wall-clock marks of the last k_vocab_sel launch (100 MHz),
+// read by wh_tune_vs_trace (profiles/vocab_sel_trace.py)
+constexpr int VS_MARKS = 10;
+__device__ unsigned long long g_vs_trace[VS_NB][VS_MARKS];
+#define VS_MARK(k)                                                                          \
+  do {                                                                                      \
+    if (threadIdx.x == 0) g_vs_trace[blockIdx.x][k] = __builtin_amdgcn_s_memrealtime();    \
+  } while (0)
+#else
+#define VS_MARK(k) \
+  do {             \
+  } while (0)
+#endif
+
+template <int D>
+__global__ __launch_bounds__(512) void k_vocab_sel(GemmArgs a, VsArgs v) {
+  constexpr int KW = 8, SW = 5, K = KW * SW * 32, TMAX = VS_TMAX;  // K 1280 (launcher)
+  constexpr int XROW = K * 2 + 16;
+  extern __shared__ __attribute__((aligned(16))) char vs_lds[];
+  float4_t* red = reinterpret_cast<float4_t*>(vs_lds + 8 * XROW);  // [TMAX tiles][KW][64]
+  float* lg = reinterpret_cast<float*>(vs_lds);                   // [8][TMAX * 16] logits (X dead)
+  MergeLds& mlds = *reinterpret_cast<MergeLds*>(vs_lds + 8 * XROW);  // red's space, after the records
+  __shared__ LpMasks fm[VS_ROWS];
+  __shared__ int s_last;
+  const DecState& s = v.s;
+  const DecOpts& o = v.o;
+  VS_MARK(0);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = lane & 15, g = lane >> 4;
+  const int nt = (a.N + 15) / 16, b = blockIdx.x, nb = gridDim.x;
+  const int t0 = (int)((int64_t)b * nt / nb), t1 = (int)((int64_t)(b + 1) * nt / nb), ntl = t1 - t0;
+  const half_t* W = reinterpret_cast<const half_t*>(a.W);
+  const int kb = wave * SW * 32;
+  // 1. the window's state first (its loads retire first), then the LayerNorm operands,
+  // then the first D - 1 weight tiles
+  const int done = s.done[0], len = s.len[0], sb = s.sample_begin[0];
+  auto load_tile = [&](int tl, Frag<half_t> (&wf)[SW]) {
+    const int tile = t0 + min(tl, ntl - 1);
+    const half_t* wp = W + (int64_t)min(tile * 16 + r, a.N - 1) * K + kb + 8 * g;
+#pragma unroll
+    for (int s2 = 0; s2 < SW; ++s2) frag_load_stream(wf[s2], wp + s2 * 32);
+  };
+  constexpr int CPLM = 5;
+  const int row = wave;
+  const bool lnrow = row < a.M;
+  float4_t xv[CPLM], gv[CPLM], bv[CPLM];
+  if (lnrow) {
+    const float* xr = a.xf32 + (int64_t)row * K;
+#pragma unroll
+    for (int i = 0; i < CPLM; ++i) {
+      const int c = lane + 64 * i;
+      xv[i] = load4f(xr + 4 * c);
+      gv[i] = load4f(a.ln_g + 4 * c);
+      bv[i] = load4f(a.ln_b + 4 * c);
+    }
+  }
+  Frag<half_t> wf[D][SW];
+#pragma unroll
+  for (int t = 0; t < D - 1; ++t) load_tile(t, wf[t]);
+  if (done) {  // a finished window: no selection; its rows are re-embedded (merge_window)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (b == 0) merge_window<512, false>(s, o, v.em, 0, tid, mlds);
+    return;
+  }
+  VS_MARK(1);
+  // 2. this row's history facts (decoding.py:503-508), in flight during the projection
+  const int tb = o.ts_begin, V = o.V;
+  const int c0 = t0 * 16, c1 = min(t1 * 16, a.N);
+  int hv[7], h1 = 0, h2 = 0;
+  unsigned sw[4] = {0u, 0u, 0u, 0u};  // suppress words of this lane's columns
+  unsigned long long seed = 0;
+  if (lnrow) {
+    const int* hist = s.hist + (int64_t)row * s.hctx;
+#pragma unroll
+    for (int i = 0; i < 7; ++i) hv[i] = hist[min(sb + lane + 64 * i, max(len - 1, 0))];
+    h1 = hist[max(len - 1, 0)];
+    h2 = hist[max(len - 2, 0)];
+    if (o.suppress)
+#pragma unroll
+      for (int u = 0; u < 4; ++u) sw[u] = o.suppress[min(c0 + lane + 64 * u, c1 - 1) >> 5];
+    seed = s.seed[0];
+  }
+  // 3. the final LayerNorm (k_vocab1's prologue) and the projection
+  {
+    half_t* dst = reinterpret_cast<half_t*>(vs_lds + row * XROW);
+    if (!lnrow) {
+      for (int c = lane; c < K / 4; c += 64) store4(dst + 4 * c, 0.f, 0.f, 0.f, 0.f);
+    } else {
+      float sm = 0.f;
+#pragma unroll
+      for (int i = 0; i < CPLM; ++i) sm += xv[i][0] + xv[i][1] + xv[i][2] + xv[i][3];
+      const float mean = wave_sum(sm) / (float)K;
+      float q = 0.f;
+#pragma unroll
+      for (int i = 0; i < CPLM; ++i)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float d = xv[i][e] - mean;
+          q += d * d;
+        }
+      const float rstd = rsqrtf(wave_sum(q) / (float)K + a.ln_eps);
+#pragma unroll
+      for (int i = 0; i < CPLM; ++i) {
+        const float4_t x4 = xv[i];
+        store4(dst + 4 * (lane + 64 * i), (x4[0] - mean) * rstd * gv[i][0] + bv[i][0],
+               (x4[1] - mean) * rstd * gv[i][1] + bv[i][1], (x4[2] - mean) * rstd * gv[i][2] + bv[i][2],
+               (x4[3] - mean) * rstd * gv[i][3] + bv[i][3]);
+      }
+    }
+  }
+  __syncthreads();
+  Frag<half_t> xf[SW];
+#pragma unroll
+  for (int s2 = 0; s2 < SW; ++s2)
+    frag_load(xf[s2], reinterpret_cast<const half_t*>(vs_lds + min(r, 7) * XROW) + kb + s2 * 32 + 8 * g);
+#pragma unroll
+  for (int t = 0; t < TMAX; ++t) {
+    if (t + D - 1 < TMAX) load_tile(t + D - 1, wf[(t + D - 1) % D]);
+    float4_t acc = (float4_t){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s2 = 0; s2 < SW; ++s2) mfma_step(acc, wf[t % D][s2], xf[s2]);
+    if (t < ntl) red[(t * KW + wave) * 64 + lane] = acc;
+  }
+  VS_MARK(2);
+  // the row's masks (its history loads have long landed)
+  if (lnrow) {
+    int pm = -1, pt = -1;
+#pragma unroll
+    for (int i = 0; i < 7; ++i) {
+      const int p = sb + lane + 64 * i;
+      if (p < len && hv[i] >= tb) { pm = p; pt = hv[i]; }
+    }
+#pragma unroll
+    for (int o2 = 32; o2 > 0; o2 >>= 1) {
+      const int op = __shfl_xor(pm, o2, 64), ot = __shfl_xor(pt, o2, 64);
+      if (op > pm) { pm = op; pt = ot; }
+    }
+    const int nseq = len - sb;
+    const bool last_ts = nseq >= 1 && h1 >= tb, penult_ts = nseq < 2 || h2 >= tb, first = len == sb;
+    const LpMasks f = lp_masks(o, last_ts, penult_ts, first, pm >= 0 ? pt : -1);
+    if (lane == 0) fm[row] = f;
+  }
+  __syncthreads();
+  // 4. the logits of this workgroup's columns: the 8 eighths in wave order (k_vocab1)
+  constexpr int LGW = TMAX * 16;
+  for (int i = tid; i < ntl * 64; i += 512) {
+    const int tl = i >> 6, ln = i & 63, rr = ln & 15;
+    float4_t x4 = red[(tl * KW) * 64 + ln];
+#pragma unroll
+    for (int w2 = 1; w2 < KW; ++w2) x4 += red[(tl * KW + w2) * 64 + ln];
+    if (rr < a.M) *reinterpret_cast<float4_t*>(lg + rr * LGW + tl * 16 + 4 * (ln >> 4)) = x4;
+  }
+  __syncthreads();
+  VS_MARK(3);
+  // 5. one wave per row: a record per part of this workgroup's columns
+  const int need = s.G + 1;
+  if (lnrow) {
+    const LpMasks f = fm[row];
+    const unsigned long long key =
+        splitmix64(seed ^ ((unsigned long long)row << 40) ^ ((unsigned long long)len << 20));
+#pragma unroll
+    for (int part = 0; part < 2; ++part) {
+      const int lo = part ? max(c0, tb) : c0, hi = part ? c1 : min(c1, tb);
+      if (lo >= hi) continue;
+      const auto rs = wt_rsrc(v.rec + ((int64_t)(row * 2 + part) * VS_NB + b) * VS_REC);
+      float x[4];
+      float mx = -INFINITY;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int i = c0 + lane + 64 * u;
+        x[u] = -INFINITY;
+        if (i >= lo && i < hi) {
+          bool kill = (sw[u] >> (i & 31)) & 1u;
+#pragma unroll
+          for (int q = 0; q < 5; ++q) kill |= i == f.kid[q];
+#pragma unroll
+          for (int q = 0; q < 4; ++q) kill |= (i >= f.mlo[q] && i < f.mhi[q]);
+          if (!kill) x[u] = lg[row * LGW + lane + 64 * u];
+        }
+        mx = fmaxf(mx, x[u]);
+      }
+      mx = wave_max(mx);
+      float se = 0.f;
+      if (mx > -INFINITY) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) se += __expf(x[u] - mx);
+      }
+      se = wave_sum(se);
+      if (lane == 0) { wt_store1(rs, 0, mx); wt_store1(rs, 4, se); }
+      if (!o.beam) {
+        float bvv = -INFINITY, gvv = -INFINITY, gx = -INFINITY;
+        int bi = 0x7fffffff, gi = 0x7fffffff;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int i = c0 + lane + 64 * u;
+          if (i < lo || i >= hi) continue;
+          if (better(x[u], i, bvv, bi)) { bvv = x[u]; bi = i; }
+          if (o.temperature > 0.f && x[u] != -INFINITY) {
+            const unsigned long long z = splitmix64(key + (unsigned long long)i);
+            const float uu = ((float)(z >> 40) + 0.5f) * (1.0f / 16777216.0f);
+            const float gsc = x[u] / o.temperature - logf(-logf(uu));
+            if (better(gsc, i, gvv, gi)) { gvv = gsc; gi = i; gx = x[u]; }
+          }
+        }
+        wave_argbest(bvv, bi);
+        const int mine = gi;
+        const float myx = gx;
+        wave_argbest(gvv, gi);
+        const unsigned long long own = __ballot(mine == gi && gi != 0x7fffffff);
+        const float gxw = own ? __shfl(myx, __ffsll((long long)own) - 1, 64) : -INFINITY;
+        if (lane == 0) {
+          wt_store1(rs, 8, bvv); wt_store1(rs, 12, __builtin_bit_cast(float, bi));
+          wt_store1(rs, 16, gvv); wt_store1(rs, 20, __builtin_bit_cast(float, gi));
+          wt_store1(rs, 24, gi != 0x7fffffff ? gxw : -INFINITY);
+        }
+      } else {
+        unsigned taken = 0u;
+        for (int q = 0; q < need; ++q) {
+          float bvv = -INFINITY;
+          int bi = 0x7fffffff;
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const int i = c0 + lane + 64 * u;
+            if (i >= lo && i < hi && !((taken >> u) & 1u) && better(x[u], i, bvv, bi)) { bvv = x[u]; bi = i; }
+          }
+          const int mine = bi;
+          wave_argbest(bvv, bi);
+          if (mine == bi && bi != 0x7fffffff) taken |= 1u << ((bi - c0 - lane) / 64);
+          if (lane == 0) {
+            wt_store1(rs, 4 * (VS_TV + q), bvv);
+            wt_store1(rs, 4 * (VS_TI + q), __builtin_bit_cast(float, bi));
+          }
+        }
+      }
+    }
+  }
+  // 6. arrival: every storing wave drains its records, one agent add per workgroup
+  VS_MARK(4);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  VS_MARK(5);
+  if (tid == 0) s_last = __hip_atomic_fetch_add(v.cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nb - 1;
+  __syncthreads();
+  VS_MARK(6);
+  if (!s_last) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");  // no instruction: keeps the loads below the add
+  if (tid == 0) __hip_atomic_store(v.cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  // 7. the combine, one wave per row: text records of the workgroups with columns below
+  // timestamp_begin (lane j: workgroups j, j + 64, ...), timestamp records of those above
+  if (lnrow) {
+    auto col0 = [&](int wb) { return (int)((int64_t)wb * nt / nb) * 16; };
+    auto col1 = [&](int wb) { return min((int)((int64_t)(wb + 1) * nt / nb) * 16, a.N); };
+    const auto rsr = wt_rsrc(v.rec);
+    auto ld = [&](int part, int wb, int word) -> float {
+      return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                           rsr, (((row * 2 + part) * VS_NB + wb) * VS_REC + word) * 4, 0, 16));
+    };
+    // the first workgroup with timestamp columns (<= 64 of them: launcher)
+    int bts = nb;
+    for (int bb = lane; bb < nb; bb += 64)
+      if (col1(bb) > tb) bts = min(bts, bb);
+#pragma unroll
+    for (int o2 = 32; o2 > 0; o2 >>= 1) bts = min(bts, __shfl_xor(bts, o2, 64));
+    // record k of this lane: k < 4 text (workgroup lane + 64 k), k == 4 timestamps
+    // (workgroup bts + lane)
+    constexpr int NR = 5;
+    auto rwb = [&](int k) { return k < 4 ? lane + 64 * k : bts + lane; };
+    bool val[NR];
+    float rmx[NR], rse[NR];
+#pragma unroll
+    for (int k = 0; k < NR; ++k) {
+      const int wb = rwb(k), part = k == 4;
+      val[k] = wb < nb && (part ? col1(wb) > tb && col0(wb) < a.N : col0(wb) < min(tb, a.N));
+      const int wc = val[k] ? wb : 0;
+      rmx[k] = ld(part, wc, 0);
+      rse[k] = ld(part, wc, 1);
+      if (!val[k]) rmx[k] = -INFINITY;
+    }
+    float m = -INFINITY, mtx = -INFINITY, mts = -INFINITY;
+#pragma unroll
+    for (int k = 0; k < NR; ++k) {
+      m = fmaxf(m, rmx[k]);
+      if (k < 4) mtx = fmaxf(mtx, rmx[k]);
+      else mts = fmaxf(mts, rmx[k]);
+    }
+    m = wave_max(m);
+    mtx = wave_max(mtx);
+    mts = wave_max(mts);
+    bool text_killed = false;
+    if (o.timestamps) {
+      float st0 = 0.f, sts = 0.f;
+#pragma unroll
+      for (int k = 0; k < NR; ++k)
+        if (rmx[k] > -INFINITY) {
+          st0 += rse[k] * __expf(rmx[k] - m);
+          if (k == 4) sts += rse[k] * __expf(rmx[k] - mts);
+        }
+      st0 = wave_sum(st0);
+      sts = wave_sum(sts);
+      const float lS0 = logf(st0);
+      const float lts = mts > -INFINITY ? (mts - m) - lS0 : -INFINITY;
+      const float ltx = mtx > -INFINITY ? (mtx - m) - lS0 : -INFINITY;
+      const float ts_lp = lts > -INFINITY ? lts + logf(sts) : -INFINITY;
+      text_killed = ts_lp > ltx;
+      if (text_killed) m = mts;
+    }
+    bool kept[NR];
+#pragma unroll
+    for (int k = 0; k < NR; ++k) kept[k] = val[k] && (!text_killed || k == 4);
+    float se = 0.f;
+#pragma unroll
+    for (int k = 0; k < NR; ++k)
+      if (kept[k] && rmx[k] > -INFINITY) se += rse[k] * __expf(rmx[k] - m);
+    const float logS = logf(wave_sum(se));
+    const auto rcv = wt_rsrc(s.cand_val + (int64_t)row * KC), rci = wt_rsrc(s.cand_idx + (int64_t)row * KC);
+    if (!o.beam) {
+      const bool samp = o.temperature > 0.f;
+      float bvv = -INFINITY, bx = -INFINITY;
+      int bi = 0x7fffffff;
+#pragma unroll
+      for (int k = 0; k < NR; ++k) {
+        if (!kept[k]) continue;
+        const int wb = rwb(k), part = k == 4;
+        const float cv = ld(part, wb, samp ? 4 : 2);
+        const int ci = __builtin_bit_cast(int, ld(part, wb, samp ? 5 : 3));
+        const float cx = samp ? ld(part, wb, 6) : cv;
+        if (better(cv, ci, bvv, bi)) { bvv = cv; bi = ci; bx = cx; }
+      }
+      const int mine = bi;
+      const float myx = bx;
+      wave_argbest(bvv, bi);
+      const unsigned long long own = __ballot(mine == bi && bi != 0x7fffffff);
+      const float wx = own ? __shfl(myx, __ffsll((long long)own) - 1, 64) : -INFINITY;
+      if (lane == 0 && bi != 0x7fffffff) {
+        wt_store1(rci, 0, __builtin_bit_cast(float, bi));
+        wt_store1(rcv, 0, (wx - m) - logS);
+      }
+    } else {
+      // each lane's kept records' sorted lists; `need` rounds take the best head
+      float tv[NR][KC];
+      int ti[NR][KC];
+#pragma unroll
+      for (int k = 0; k < NR; ++k) {
+        const int wb = kept[k] ? rwb(k) : 0, part = k == 4;
+#pragma unroll
+        for (int q = 0; q < KC; ++q) {
+          tv[k][q] = -INFINITY;
+          ti[k][q] = 0x7fffffff;
+          if (q < need) {
+            tv[k][q] = ld(part, wb, VS_TV + q);
+            ti[k][q] = __builtin_bit_cast(int, ld(part, wb, VS_TI + q));
+          }
+          if (!kept[k]) { tv[k][q] = -INFINITY; ti[k][q] = 0x7fffffff; }
+        }
+      }
+      int hd[NR] = {0, 0, 0, 0, 0};
+      for (int q = 0; q < need; ++q) {
+        float hv2 = -INFINITY;
+        int hi2 = 0x7fffffff, hk = -1;
+#pragma unroll
+        for (int k = 0; k < NR; ++k) {
+          float cv = -INFINITY;
+          int ci = 0x7fffffff;
+#pragma unroll
+          for (int qq = 0; qq < KC; ++qq)
+            if (qq == hd[k]) { cv = tv[k][qq]; ci = ti[k][qq]; }
+          if (hd[k] < need && better(cv, ci, hv2, hi2)) { hv2 = cv; hi2 = ci; hk = k; }
+        }
+        float bvv = hv2;
+        int bi = hi2;
+        wave_argbest(bvv, bi);
+        if (bi == hi2 && bi != 0x7fffffff && hk >= 0) {
+#pragma unroll
+          for (int k = 0; k < NR; ++k)
+            if (k == hk) ++hd[k];
+        }
+        if (lane == 0) {
+          wt_store1(rcv, 4 * q, (bvv - m) - logS);
+          wt_store1(rci, 4 * q, __builtin_bit_cast(float, bi));
+        }
+      }
+    }
+  }
+  // 8. the window's candidate merge, with the candidates just written (sc1 loads)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  VS_MARK(7);
+  merge_window<512, true>(s, o, v.em, 0, tid, mlds);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  VS_MARK(8);
+}
+
+#if WH_TUNING
+extern "C" int wh_tune_vs_trace(unsigned long long* out) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_vs_trace), sizeof(g_vs_trace)) == hipSuccess ? 0 : -1;
+}
+#endif
+
+// one window's tail in one launch; -1 when the shape is not the single-window fp16 step
+bool vocab_select_on() {
+  static const bool on = [] {  // tuning build only: WHISPER_HIP_VOCAB_SEL=1
+    const char* e = tune_env("WHISPER_HIP_VOCAB_SEL");
+    return e && e[0] == '1';
+  }();
+  return on;
+}
+
+int launch_vocab_select(const GemmArgs& a, const DecState& s, const DecOpts& o, const MergeEmbed& em, float* rec,
+                        int* cnt, hipStream_t st) {
+  const int nt = (a.N + 15) / 16;
+  if (!vocab_select_on() || !rec || !cnt || !a.xf32 || a.K != 1280 || a.bias || a.M < 1 || a.M > VS_ROWS || a.M != s.G ||
+      s.G > MG_MAXG || nt > VS_NB * VS_TMAX || nt < VS_NB || o.ts_begin <= 0 || o.ts_begin > a.N || a.N != o.V ||
+      a.N - o.ts_begin > 64 * 16 * (nt / VS_NB) - 16)  // <= 64 workgroups hold timestamp columns
+    return -1;
+  constexpr int D = 6;
+  const int lds = 8 * (1280 * 2 + 16) + VS_TMAX * 8 * 64 * 16;
+  static_assert(sizeof(MergeLds) <= VS_TMAX * 8 * 64 * 16, "merge scratch inside the reduction space");
+  // (the dynamic size itself: the kernel's static LDS counts against the 160 KB too)
+  static bool attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_vocab_sel<D>),
+                                         hipFuncAttributeMaxDynamicSharedMemorySize, lds) == hipSuccess;
+  if (!attr) return -5;
+  VsArgs v;
+  v.s = s; v.o = o; v.em = em; v.rec = rec; v.cnt = cnt;
+  k_vocab_sel<D><<<VS_NB, 512, lds, st>>>(a, v);
+  return 0;
 }
 
 // ------------------------------------------------------------ per-step ABI state updates

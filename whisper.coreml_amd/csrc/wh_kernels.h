@@ -122,6 +122,13 @@ struct MergeEmbed {
   int n = 0, pmax = 0, half = 0;
 };
 void launch_merge(const DecState& s, const DecOpts& o, int nwin, hipStream_t st, const MergeEmbed& em = MergeEmbed());
+// the single-window step's whole token tail (vocabulary projection with the final
+// LayerNorm, selection, merge) in one launch; -1 when the shape does not fit it
+struct GemmArgs;
+bool vocab_select_on();
+int launch_vocab_select(const GemmArgs& a, const DecState& s, const DecOpts& o, const MergeEmbed& em, float* rec,
+                        int* cnt, hipStream_t st);
+constexpr size_t VS_REC_FLOATS = 8 * 2 * 256 * 32;  // k_vocab_sel records [rows][part][workgroup][32]
 // token selection + candidate merge of one update: one k_logit_part launch whose last
 // row combiner of each window runs the merge (round 4), or k_logit_* then k_merge
 void launch_select_merge(float* logits, int ldl, const DecState& s, const DecOpts& o, int nwin, hipStream_t st,

@@ -744,6 +744,189 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void
   }
 }
 
+// Grouped form (fp16, a window's G <= 8 beams as the G waves of one workgroup per
+// (window, head)).  Per wave the arithmetic is k_self_attn_qkv's fp16 path operation for
+// operation (same passes of 128 keys, same lane roles and orders: bit-identical outputs);
+// only where the cached K / V rows come from changes.  Beam histories form a tree: beam b
+// names beam 0's (slot, position) rows exactly on [0, d_b), d_b = the first position where
+// their ancestries differ, and never again after it.  So each pass stages beam 0's 128 K
+// and V rows in LDS once (global_load_lds, 32 KB shared by the G waves) and a lane reads a
+// key from LDS below its beam's d_b and from HBM at or above it (profiles/ancestry_probe.py:
+// at 20 windows the beams share 37-97 % of their context, 1.1-2.4 distinct rows per
+// position, where every wave streamed its own rows).  K rows are stored with their 16 B
+// chunks XOR-swizzled by (row >> 1) & 7, so lane-per-row reads of a chunk are conflict-free.
+WH_DEV void sa_glds16(const void* src, void* lds) {
+  __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)(src),
+                                   (__attribute__((address_space(3))) void*)(lds), 16, 0, 0);
+}
+
+constexpr int SA_GMAX = 8;
+template <typename T>
+__global__ __launch_bounds__(64 * SA_GMAX) void k_self_attn_grp(const float* __restrict__ part, int nsplit,
+                                                                 int64_t part_stride, const float* __restrict__ bqkv,
+                                                                 int ns, T* __restrict__ kc, T* __restrict__ vc,
+                                                                 const int* __restrict__ row_pos,
+                                                                 const int* __restrict__ anc, int G, int nbeam, int H,
+                                                                 int ctx, T* __restrict__ out, int ldo) {
+  static_assert(sizeof(T) == 2, "fp16 path");
+  __shared__ __attribute__((aligned(1024))) T kref[128 * 64];
+  __shared__ __attribute__((aligned(1024))) T vref[128 * 64];
+  __shared__ int slot_of[SA_GMAX][512];
+  __shared__ __attribute__((aligned(16))) float qs[SA_GMAX][64], vs[SA_GMAX][64], sc[SA_GMAX][128];
+  const int lane = threadIdx.x & 63, sl = threadIdx.x >> 6;
+  const int h = blockIdx.x % H, w = blockIdx.x / H, row = w * G + sl;
+  const int* an = anc + ((int64_t)w * G + sl) * ctx;
+  const int64_t head_stride = (int64_t)ctx * 64;
+  const int64_t wbase = (int64_t)w * nbeam;
+  auto kv_off = [&](int slot, int p) -> int64_t { return ((wbase + slot) * H + h) * head_stride + (int64_t)p * 64; };
+  // the prologue of k_self_attn_qkv (one round trip: position, ancestry, q/k/v slabs)
+  const int pos = row_pos[row];
+  int sv[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) sv[i] = an[min(lane + 64 * i, ctx - 1)];
+  float qd, kd, vd;
+  {
+    const float* pr = part + (int64_t)row * 3 * ns + h * 64 + lane;
+    float a0[16], a1[16], a2[16];
+#pragma unroll
+    for (int z = 0; z < 16; ++z)
+      if (z < nsplit) {
+        a0[z] = pr[z * part_stride];
+        a1[z] = pr[z * part_stride + ns];
+        a2[z] = pr[z * part_stride + 2 * ns];
+      }
+    qd = bqkv[h * 64 + lane];
+    kd = bqkv[ns + h * 64 + lane];
+    vd = bqkv[2 * ns + h * 64 + lane];
+#pragma unroll
+    for (int z = 0; z < 16; ++z)
+      if (z < nsplit) {
+        qd += a0[z];
+        kd += a1[z];
+        vd += a2[z];
+      }
+  }
+  for (int i = 0; i < 8; ++i)
+    if (lane + 64 * i < pos) slot_of[sl][lane + 64 * i] = sv[i];
+  const int plast = max(pos - 1, 0);
+  const T qT = from_f32<T>(qd), kT = from_f32<T>(kd), vT = from_f32<T>(vd);
+  kc[kv_off(sl, pos) + lane] = kT;
+  vc[kv_off(sl, pos) + lane] = vT;
+  qs[sl][lane] = to_f32(qT);
+  vs[sl][lane] = to_f32(vT);
+  const float s_cur = wave_sum(to_f32(qT) * to_f32(kT));
+  __syncthreads();  // every beam's ancestry in LDS
+  // d: the first position where this beam's ancestry leaves beam 0's
+  int d = pos;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int p = lane + 64 * i;
+    if (p < pos && slot_of[sl][p] != slot_of[0][p]) d = min(d, p);
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) d = min(d, __shfl_xor(d, o, 64));
+  // q stays in LDS (broadcast reads in the dot products: 64 VGPRs fewer than a register copy)
+  const int kg = lane >> 3, dc = (lane & 7) * 8;
+  float m = s_cur, lsum = 0.f, o[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) o[e] = 0.f;
+  for (int p0 = 0; p0 < pos; p0 += 128) {
+    // beam 0's rows p0 .. p0 + 127 (< pos) -> LDS: 16 K and 16 V instructions of 8 rows,
+    // dealt over the G waves; lane (row r0 + lane / 8, chunk lane % 8)
+    for (int i = sl; i < 32; i += G) {
+      const int r0 = (i & 15) * 8, r = r0 + (lane >> 3), p = p0 + r;
+      if (p <= plast) {
+        const int pc = lane & 7;
+        if (i < 16) {  // K: physical chunk pc holds logical chunk pc ^ ((r >> 1) & 7)
+          sa_glds16(kc + kv_off(slot_of[0][p], p) + 8 * (pc ^ ((r >> 1) & 7)), kref + r0 * 64);
+        } else {
+          sa_glds16(vc + kv_off(slot_of[0][p], p) + 8 * pc, vref + r0 * 64);
+        }
+      }
+    }
+    // this beam's own rows at or past d, straight from HBM into registers
+    const int pa = min(p0 + lane, plast), pb = min(p0 + 64 + lane, plast);
+    const bool la = pa < d, lb = pb < d;
+    Frag<T> ka[8], kb[8], vf[16];
+    if (!la) {
+      const T* ra = kc + kv_off(slot_of[sl][pa], pa);
+#pragma unroll
+      for (int c = 0; c < 8; ++c) frag_load(ka[c], ra + 8 * c);
+    }
+    if (!lb) {
+      const T* rb = kc + kv_off(slot_of[sl][pb], pb);
+#pragma unroll
+      for (int c = 0; c < 8; ++c) frag_load(kb[c], rb + 8 * c);
+    }
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      const int pc = min(p0 + kg + 8 * u, plast);
+      if (pc >= d) frag_load(vf[u], vc + kv_off(slot_of[sl][pc], pc) + dc);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();  // the staged rows of every wave
+    if (la) {
+      const int r = pa - p0, sw = (r >> 1) & 7;
+#pragma unroll
+      for (int c = 0; c < 8; ++c) ka[c].v = *reinterpret_cast<const half8_t*>(kref + r * 64 + 8 * (c ^ sw));
+    }
+    if (lb) {
+      const int r = pb - p0, sw = (r >> 1) & 7;
+#pragma unroll
+      for (int c = 0; c < 8; ++c) kb[c].v = *reinterpret_cast<const half8_t*>(kref + r * 64 + 8 * (c ^ sw));
+    }
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      const int pc = min(p0 + kg + 8 * u, plast);
+      if (pc < d) vf[u].v = *reinterpret_cast<const half8_t*>(vref + (pc - p0) * 64 + dc);
+    }
+    float sa = 0.f, sb = 0.f;
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+      const float4_t q0 = *reinterpret_cast<const float4_t*>(&qs[sl][8 * c]);
+      const float4_t q1 = *reinterpret_cast<const float4_t*>(&qs[sl][8 * c + 4]);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float qe = e < 4 ? q0[e] : q1[e - 4];
+        sa += qe * to_f32(ka[c].v[e]);
+        sb += qe * to_f32(kb[c].v[e]);
+      }
+    }
+    const bool va = p0 + lane < pos, vb = p0 + 64 + lane < pos;
+    const float mp = wave_max(fmaxf(va ? sa : -INFINITY, vb ? sb : -INFINITY));
+    const float mn = fmaxf(m, mp), scale = __expf(m - mn);
+    m = mn;
+    const float ea = va ? __expf(sa - m) : 0.f, eb = vb ? __expf(sb - m) : 0.f;
+    lsum = lsum * scale + wave_sum(ea + eb);
+    sc[sl][lane] = ea;
+    sc[sl][64 + lane] = eb;
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] *= scale;
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      const float pw = sc[sl][kg + 8 * u];  // 0 past the end
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o[e] += pw * to_f32(vf[u].v[e]);
+    }
+    __syncthreads();  // the staged rows are read: the next pass may overwrite them
+  }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    o[e] += __shfl_xor(o[e], 8, 64);
+    o[e] += __shfl_xor(o[e], 16, 64);
+    o[e] += __shfl_xor(o[e], 32, 64);
+  }
+  if (kg == 0) {
+    const float e_cur = __expf(s_cur - m), inv = 1.f / (lsum + e_cur);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] = (o[e] + e_cur * vs[sl][dc + e]) * inv;
+    T* op = out + (int64_t)row * ldo + h * 64 + dc;
+    store4(op, o[0], o[1], o[2], o[3]);
+    store4(op + 4, o[4], o[5], o[6], o[7]);
+  }
+}
+
 template <typename T>
 int launch_self_attn_qkv(const float* part, int nsplit, int64_t part_stride, const float* bqkv, int ns, T* kc, T* vc,
                           const int* rw, const int* rs, const int* rp, const int* anc, int anc_beams, int nbeam, int H,
@@ -753,6 +936,21 @@ int launch_self_attn_qkv(const float* part, int nsplit, int64_t part_stride, con
   // fp32 slabs only: the (row, head) wave reads its q / k / v columns lane per element
   // (an fp16-slab form measured 8.7 -> 13.9 us per launch)
   if (anc_beams < 1 || rows % anc_beams || nsplit > 16 || slab_half) return -1;
+  // fp16 beams, tuning build only (WHISPER_HIP_SA_GRP=1): the grouped form, same arithmetic
+  // per row.  Measured slower at every context length (20 windows: step 3.456 -> 3.655 ms
+  // at 12 tokens, 3.834 -> 4.114 at 220, profiles/r04/self_attn_grp_ab.txt): at 238 VGPRs a
+  // CU holds one 5-wave workgroup, so the 400 (window, head) workgroups run in two rounds
+  static const bool grp = [] {
+    const char* e = tune_env("WHISPER_HIP_SA_GRP");
+    return e && e[0] == '1';
+  }();
+  if constexpr (sizeof(T) == 2) {
+    if (grp && anc_beams >= 2 && anc_beams <= SA_GMAX && ctx <= 512) {
+      k_self_attn_grp<T><<<(rows / anc_beams) * H, 64 * anc_beams, 0, st>>>(part, nsplit, part_stride, bqkv, ns, kc, vc,
+                                                                            rp, anc, anc_beams, nbeam, H, ctx, out, ldo);
+      return 0;
+    }
+  }
   k_self_attn_qkv<T><<<rows * H, 64, 0, st>>>(part, nsplit, part_stride, bqkv, ns, kc, vc, rw, rs, rp, anc, anc_beams,
                                              nbeam, H, ctx, out, ldo);
   return 0;

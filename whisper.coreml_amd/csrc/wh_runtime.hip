@@ -189,6 +189,8 @@ struct Ctx : public wh_ctx {
   int *st_row_win, *st_row_slot, *st_win_row0, *st_win_nrows, *st_win_slot;
   static constexpr int P1_SLABS = 2048;  // k_proj1 split-K slabs: zs x 16-column tiles <= 16 x 80 at n = 1280
   float* p1_slab = nullptr;  // k_proj1 in-launch split-K slabs [zs][N/16][256]
+  float* vs_rec = nullptr;   // k_vocab_sel records
+  int* vs_cnt = nullptr;     // and its arrival counter (zero between launches)
   int* p1_cnt = nullptr;     // and arrival counters [4n/16] (zero between launches)
   float* xs_rec = nullptr;   // step cross-attention segment records [pair][XS_NSP][XREC]
   float* x2_d = nullptr;     // k_proj1 path: second residual buffer (deferred residual ping-pong)
@@ -346,6 +348,7 @@ struct Ctx : public wh_ctx {
     addA((size_t)Wcap * Gcap * KC * 4); addA((size_t)Wcap * Gcap * KC * 4);
     addA((size_t)Wcap * Gcap * LP_SLICES * LP_REC * 4); addA((size_t)Wcap * Gcap * 4);
     addA((size_t)Wcap * 4);  // window arrival counters of the merging selection
+    addA(VS_REC_FLOATS * 4); addA(64);  // single-window tail records + arrival counter
     addA(64);
     addA(64);
     addA((size_t)P1_SLABS * 256 * 4); addA((size_t)(4 * n / 16) * 4);  // k_proj1 split-K slabs + counters
@@ -383,11 +386,12 @@ struct Ctx : public wh_ctx {
     S.cand_val = fa((size_t)Wcap * Gcap * KC); S.cand_idx = ia((size_t)Wcap * Gcap * KC);
     S.lpart = fa((size_t)Wcap * Gcap * LP_SLICES * LP_REC); S.lp_cnt = ia((size_t)Wcap * Gcap);  // zeroed with the arena
     S.lpw_cnt = ia((size_t)Wcap);
+    vs_rec = fa(VS_REC_FLOATS); vs_cnt = ia(16);  // zeroed with the arena
     S.seed = (unsigned long long*)aa.take(64);
     p1_slab = fa((size_t)P1_SLABS * 256); p1_cnt = ia(4 * n / 16);  // zeroed with the arena
     xs_rec = fa((size_t)Wcap * nh * XS_NSP * XREC); xs_cnt = ia((size_t)Wcap * nh);
     x2_d = fa((size_t)8 * n);
-    if (!S.seed || !S.cand_idx || !S.lp_cnt || !S.lpw_cnt || !p1_cnt || !xs_cnt || !x2_d) return fail(-3, "activation arena overflow");
+    if (!S.seed || !S.cand_idx || !S.lp_cnt || !S.lpw_cnt || !vs_cnt || !p1_cnt || !xs_cnt || !x2_d) return fail(-3, "activation arena overflow");
     S.nw = Wcap; S.G = 1; S.ctx = CTX; S.hctx = HCTX; S.maxc = 16;
     HIPCHK(hipMalloc(&d_gmax, 64));
     d_gmax_f = (float*)(d_gmax + 4);
@@ -928,7 +932,10 @@ struct Ctx : public wh_ctx {
   // DESIGN.md §2)
   bool p1_active(int R, int n_win) const { return n_win == 1 && p1_enabled() && proj1_supported(R, ns); }
   std::string step_kernels(int n_win, int group) const override {
-    return std::string("proj=") + (p1_active(n_win * group, n_win) ? "k_proj1" : "k_proj") + ",xattn=k_xattn_seg";
+    const bool p1 = p1_active(n_win * group, n_win), h = sizeof(T) == 2;
+    return std::string("proj=") + (p1 ? "k_proj1" : "k_proj") + ",xattn=k_xattn_seg" +
+           ",self_attn=" + (p1 ? "k_self_attn" : h && group >= 2 ? "k_self_attn_grp" : "k_self_attn_qkv") +
+           ",tail=" + (p1 && h && ns == 1280 && vocab_select_on() ? "k_vocab_sel" : "vocab+k_logit_part");
   }
 
   int dec_layers_p1(int R, const int* rw, const int* rs, const int* rp, int ancG, int nwin, const int* wr0,
@@ -1205,6 +1212,15 @@ struct Ctx : public wh_ctx {
     const int R = cur_nwin * cur_G;
     TRY(dec_layers(R, st_row_win, st_row_slot, row_pos, cur_G, cur_nwin, st_win_row0, st_win_nrows, st_win_slot,
                    nullptr, nullptr, 0, true));
+    if (final_x && cur_nwin == 1 && sizeof(T) == 2) {
+      // one window (k_proj1 layers): vocabulary, selection and merge in one launch
+      GemmArgs g;
+      g.X = xn_d; g.ldx = ns; g.W = E; g.M = R; g.N = V; g.K = ns; g.out_f32 = logits; g.ldo = V;
+      g.xf32 = final_x; g.ln_g = ln_g; g.ln_b = ln_b; g.ln_eps = 1e-5f;
+      const int rc = launch_vocab_select(g, S, O, merge_embed(), vs_rec, vs_cnt, st);
+      if (rc == 0) return 0;
+      if (rc != -1) return fail(-20, "k_vocab_sel launch failed code " + std::to_string(rc));
+    }
     TRY(vocab(nullptr, R, logits));
     launch_select_merge(logits, V, S, O, cur_nwin, st, merge_embed());
     return 0;

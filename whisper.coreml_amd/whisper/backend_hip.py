@@ -401,7 +401,7 @@ class HipContext:
 
     def step_kernels(self, n_win: int, group: int) -> dict:
         """The kernels the decoder step runs for this batch shape (wh_step_kernels):
-        {"proj": ..., "xattn": ...}."""
+        {"proj", "xattn", "self_attn", "tail"}."""
         buf = ctypes.create_string_buffer(256)
         n = self.lib.wh_step_kernels(self.h, n_win, group, buf, 256)
         self._check(0 if n >= 0 else n, "wh_step_kernels")
