@@ -160,12 +160,91 @@ WH_DEV float4_t load4f(const half_t* p) {
 WH_DEV float gelu_f(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752440f)); }
 
 // ---------------------------------------------------------------- wave reductions (wave64)
+// The xor butterfly (partner lane i ^ 32, ^ 16, ^ 8, ^ 4, ^ 2, ^ 1) without LDS: the
+// permlane swaps give every lane its i ^ 32 and i ^ 16 partner (v_permlane32_swap /
+// v_permlane16_swap on two copies: one copy ends with the lower half / even rows, the
+// other with the upper half / odd rows), then DPP row rotations by 8, 4, 2, 1 — after the
+// earlier steps lanes i and i ^ 8 (then ^ 4, ^ 2) hold bit-equal values, so lane
+// (i + k) mod 16 stands in for i ^ k.  Every lane adds the same two operands as in the
+// __shfl_xor form (IEEE addition is commutative): bit-identical results, without the six
+// dependent ds_bpermute round trips through the LDS crossbar.  Full-wave execution only
+// (every caller is in wave-uniform control flow).
+template <typename V>
+WH_DEV void perm32_pair(V& a, V& b) {  // a, b = copies of v -> (lower half, upper half) values
+  asm volatile("s_nop 1\n\tv_permlane32_swap_b32 %0, %1" : "+v"(a), "+v"(b));
+}
+template <typename V>
+WH_DEV void perm16_pair(V& a, V& b) {  // a, b = copies of v -> (even rows, odd rows) values
+  asm volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %1" : "+v"(a), "+v"(b));
+}
+template <int CTRL>
+WH_DEV float dpp_f(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xf, 0xf, true));
+}
+template <int CTRL>
+WH_DEV int dpp_i(int v) {
+  return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xf, 0xf, true);
+}
+constexpr int DPP_ROR8 = 0x128, DPP_ROR4 = 0x124, DPP_ROR2 = 0x122, DPP_ROR1 = 0x121;
 WH_DEV float wave_sum(float v) {
+  float a = v, b = v;
+  perm32_pair(a, b);
+  v = a + b;
+  a = v; b = v;
+  perm16_pair(a, b);
+  v = a + b;
+  v += dpp_f<DPP_ROR8>(v);
+  v += dpp_f<DPP_ROR4>(v);
+  v += dpp_f<DPP_ROR2>(v);
+  v += dpp_f<DPP_ROR1>(v);
+  return v;
+}
+WH_DEV float wave_max(float v) {
+  // fmaxf(own, partner) as the butterfly orders it (the sign of a max of +-0 follows the
+  // operand order)
+  const int lane = __lane_id();
+  float a = v, b = v;
+  perm32_pair(a, b);
+  v = (lane & 32) ? fmaxf(b, a) : fmaxf(a, b);
+  a = v; b = v;
+  perm16_pair(a, b);
+  v = (lane & 16) ? fmaxf(b, a) : fmaxf(a, b);
+  v = fmaxf(v, dpp_f<DPP_ROR8>(v));
+  v = fmaxf(v, dpp_f<DPP_ROR4>(v));
+  v = fmaxf(v, dpp_f<DPP_ROR2>(v));
+  v = fmaxf(v, dpp_f<DPP_ROR1>(v));
+  return v;
+}
+// single butterfly steps (partner lane i ^ 8 / ^ 16 / ^ 32), same operand order as
+// `v op __shfl_xor(v, k)`: own value first
+WH_DEV float xor8_sum(float v) { return v + dpp_f<DPP_ROR8>(v); }  // (i + 8) mod 16 == i ^ 8
+WH_DEV float xor16_sum(float v) {
+  float a = v, b = v;
+  perm16_pair(a, b);
+  return (__lane_id() & 16) ? b + a : a + b;
+}
+WH_DEV float xor32_sum(float v) {
+  float a = v, b = v;
+  perm32_pair(a, b);
+  return (__lane_id() & 32) ? b + a : a + b;
+}
+WH_DEV float xor16_max(float v) {
+  float a = v, b = v;
+  perm16_pair(a, b);
+  return (__lane_id() & 16) ? fmaxf(b, a) : fmaxf(a, b);
+}
+WH_DEV float xor32_max(float v) {
+  float a = v, b = v;
+  perm32_pair(a, b);
+  return (__lane_id() & 32) ? fmaxf(b, a) : fmaxf(a, b);
+}
+// the __shfl_xor forms, for the equality test (tools/wave_reduce_check.hip)
+WH_DEV float wave_sum_xor(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
   return v;
 }
-WH_DEV float wave_max(float v) {
+WH_DEV float wave_max_xor(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
   return v;

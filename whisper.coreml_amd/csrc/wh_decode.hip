@@ -541,14 +541,36 @@ __device__ __forceinline__ void lp_slice(int j, int ns, int tb, int V, int& lo, 
   hi = (int)((int64_t)tb * (j + 1) / (ns - 1));
 }
 
-// wave-level (value desc, index asc) argbest; every lane ends with the winner
+// wave-level (value desc, index asc) argbest; every lane ends with the winner (a total
+// order: the same winner for any pairing; permlane / DPP exchanges as wave_max, wh_common.h)
 __device__ __forceinline__ void wave_argbest(float& v, int& idx) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    const float ov = __shfl_xor(v, o, 64);
-    const int oi = __shfl_xor(idx, o, 64);
-    if (better(ov, oi, v, idx)) { v = ov; idx = oi; }
+  {
+    float a = v, b = v;
+    int ia = idx, ib = idx;
+    perm32_pair(a, b);
+    perm32_pair(ia, ib);
+    const bool t = (b > a) | ((b == a) & (ib < ia));  // better(b, a) without a branch: full EXEC below
+    v = t ? b : a;
+    idx = t ? ib : ia;
   }
+  {
+    float a = v, b = v;
+    int ia = idx, ib = idx;
+    perm16_pair(a, b);
+    perm16_pair(ia, ib);
+    const bool t = (b > a) | ((b == a) & (ib < ia));  // better(b, a) without a branch: full EXEC below
+    v = t ? b : a;
+    idx = t ? ib : ia;
+  }
+  auto step = [&](float ov, int oi) {
+    const bool t = (ov > v) | ((ov == v) & (oi < idx));
+    v = t ? ov : v;
+    idx = t ? oi : idx;
+  };
+  step(dpp_f<DPP_ROR8>(v), dpp_i<DPP_ROR8>(idx));
+  step(dpp_f<DPP_ROR4>(v), dpp_i<DPP_ROR4>(idx));
+  step(dpp_f<DPP_ROR2>(v), dpp_i<DPP_ROR2>(idx));
+  step(dpp_f<DPP_ROR1>(v), dpp_i<DPP_ROR1>(idx));
 }
 
 template <int NS, bool WT>
@@ -1058,8 +1080,9 @@ struct VsArgs {
   int* cnt;    // the launch's arrival counter (zero between launches)
 };
 constexpr int VS_ROWS = 8, VS_NB = 256, VS_REC = 32, VS_TMAX = 13;
-// record words: 0 mx, 1 se, 2 bv, 3 bi, 4 gv, 5 gi, 6 gx, 8.. tv[KC], 8 + KC.. ti[KC]
-constexpr int VS_TV = 8, VS_TI = 8 + KC;
+// record words: 0 mx, 1 se, 2 bv, 3 bi, 4 gv, 5 gi, 6 gx, 8.. tv[KC], 20.. ti[KC] (the first
+// 8 of each list 16-byte aligned: two b128 loads)
+constexpr int VS_TV = 8, VS_TI = 20;
 static_assert(VS_TI + KC <= VS_REC, "record size");
 
 #if WH_TUNING
@@ -1121,11 +1144,6 @@ __global__ __launch_bounds__(512) void k_vocab_sel(GemmArgs a, VsArgs v) {
   Frag<half_t> wf[D][SW];
 #pragma unroll
   for (int t = 0; t < D - 1; ++t) load_tile(t, wf[t]);
-  if (done) {  // a finished window: no selection; its rows are re-embedded (merge_window)
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if (b == 0) merge_window<512, false>(s, o, v.em, 0, tid, mlds);
-    return;
-  }
   VS_MARK(1);
   // 2. this row's history facts (decoding.py:503-508), in flight during the projection
   const int tb = o.ts_begin, V = o.V;
@@ -1186,6 +1204,16 @@ __global__ __launch_bounds__(512) void k_vocab_sel(GemmArgs a, VsArgs v) {
     if (t < ntl) red[(t * KW + wave) * 64 + lane] = acc;
   }
   VS_MARK(2);
+  // a finished window (the decode's last no-op steps): no selection; its rows are
+  // re-embedded (merge_window).  Checked only now, so that nothing of the projection's
+  // load stream waits on the window state.
+  if (done) {
+    if (b == 0) {
+      __syncthreads();  // every wave's X fragments are read: the merge scratch may overlap
+      merge_window<512, false>(s, o, v.em, 0, tid, mlds);
+    }
+    return;
+  }
   // the row's masks (its history loads have long landed)
   if (lnrow) {
     int pm = -1, pt = -1;
@@ -1326,19 +1354,38 @@ __global__ __launch_bounds__(512) void k_vocab_sel(GemmArgs a, VsArgs v) {
 #pragma unroll
     for (int o2 = 32; o2 > 0; o2 >>= 1) bts = min(bts, __shfl_xor(bts, o2, 64));
     // record k of this lane: k < 4 text (workgroup lane + 64 k), k == 4 timestamps
-    // (workgroup bts + lane)
+    // (workgroup bts + lane); every word the combine reads is loaded here, in one round trip
     constexpr int NR = 5;
     auto rwb = [&](int k) { return k < 4 ? lane + 64 * k : bts + lane; };
+    auto ld4 = [&](int part, int wb, int word) -> float4_t {
+      return __builtin_bit_cast(float4_t, __builtin_amdgcn_raw_buffer_load_b128(
+                                              rsr, (((row * 2 + part) * VS_NB + wb) * VS_REC + word) * 4, 0, 16));
+    };
     bool val[NR];
     float rmx[NR], rse[NR];
+    float4_t w0[NR], w1[NR], tq0[NR], tq1[NR], iq0[NR], iq1[NR];
+    float tv8[NR], ti8[NR];
 #pragma unroll
     for (int k = 0; k < NR; ++k) {
       const int wb = rwb(k), part = k == 4;
       val[k] = wb < nb && (part ? col1(wb) > tb && col0(wb) < a.N : col0(wb) < min(tb, a.N));
       const int wc = val[k] ? wb : 0;
-      rmx[k] = ld(part, wc, 0);
-      rse[k] = ld(part, wc, 1);
-      if (!val[k]) rmx[k] = -INFINITY;
+      w0[k] = ld4(part, wc, 0);
+      if (o.beam) {
+        tq0[k] = ld4(part, wc, VS_TV);
+        tq1[k] = ld4(part, wc, VS_TV + 4);
+        iq0[k] = ld4(part, wc, VS_TI);
+        iq1[k] = ld4(part, wc, VS_TI + 4);
+        tv8[k] = ld(part, wc, VS_TV + 8);
+        ti8[k] = ld(part, wc, VS_TI + 8);
+      } else {
+        w1[k] = ld4(part, wc, 4);
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < NR; ++k) {
+      rmx[k] = val[k] ? w0[k][0] : -INFINITY;
+      rse[k] = w0[k][1];
     }
     float m = -INFINITY, mtx = -INFINITY, mts = -INFINITY;
 #pragma unroll
@@ -1384,10 +1431,9 @@ __global__ __launch_bounds__(512) void k_vocab_sel(GemmArgs a, VsArgs v) {
 #pragma unroll
       for (int k = 0; k < NR; ++k) {
         if (!kept[k]) continue;
-        const int wb = rwb(k), part = k == 4;
-        const float cv = ld(part, wb, samp ? 4 : 2);
-        const int ci = __builtin_bit_cast(int, ld(part, wb, samp ? 5 : 3));
-        const float cx = samp ? ld(part, wb, 6) : cv;
+        const float cv = samp ? w1[k][0] : w0[k][2];
+        const int ci = __builtin_bit_cast(int, samp ? w1[k][1] : w0[k][3]);
+        const float cx = samp ? w1[k][2] : cv;
         if (better(cv, ci, bvv, bi)) { bvv = cv; bi = ci; bx = cx; }
       }
       const int mine = bi;
@@ -1405,16 +1451,13 @@ __global__ __launch_bounds__(512) void k_vocab_sel(GemmArgs a, VsArgs v) {
       int ti[NR][KC];
 #pragma unroll
       for (int k = 0; k < NR; ++k) {
-        const int wb = kept[k] ? rwb(k) : 0, part = k == 4;
 #pragma unroll
         for (int q = 0; q < KC; ++q) {
-          tv[k][q] = -INFINITY;
-          ti[k][q] = 0x7fffffff;
-          if (q < need) {
-            tv[k][q] = ld(part, wb, VS_TV + q);
-            ti[k][q] = __builtin_bit_cast(int, ld(part, wb, VS_TI + q));
-          }
-          if (!kept[k]) { tv[k][q] = -INFINITY; ti[k][q] = 0x7fffffff; }
+          const float x = q < 4 ? tq0[k][q] : q < 8 ? tq1[k][q - 4] : tv8[k];
+          const float xi = q < 4 ? iq0[k][q] : q < 8 ? iq1[k][q - 4] : ti8[k];
+          const bool ok = kept[k] && q < need;
+          tv[k][q] = ok ? x : -INFINITY;
+          ti[k][q] = ok ? __builtin_bit_cast(int, xi) : 0x7fffffff;
         }
       }
       int hd[NR] = {0, 0, 0, 0, 0};

@@ -282,8 +282,8 @@ __global__ __launch_bounds__(64 * ENC_NW) void k_attn_enc(const T* __restrict__ 
       for (int kt = 0; kt < 4; ++kt)
 #pragma unroll
         for (int j = 0; j < 4; ++j) mx = fmaxf(mx, sc[t][kt][j]);
-      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      mx = xor16_max(mx);
+      mx = xor32_max(mx);
       const float m_new = fmaxf(m_run[t], mx);
       alpha[t] = hw_exp2((m_run[t] - m_new) * LOG2E);
       // p = 2^(s log2e - m log2e): one fma per score; the row sum in pairs (packed adds)
@@ -300,8 +300,8 @@ __global__ __launch_bounds__(64 * ENC_NW) void k_attn_enc(const T* __restrict__ 
           pf[t][kt >> 1].v[(kt & 1) * 4 + j + 1] = from_f32<T>(p1);
         }
       float ps = ps2[0] + ps2[1];
-      ps += __shfl_xor(ps, 16, 64);
-      ps += __shfl_xor(ps, 32, 64);
+      ps = xor16_sum(ps);
+      ps = xor32_sum(ps);
       l_run[t] = l_run[t] * alpha[t] + ps;
       m_run[t] = m_new;
     }
@@ -445,9 +445,9 @@ __global__ __launch_bounds__(64) void k_self_attn(const T* __restrict__ q, int l
     }
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
-      o[e] += __shfl_xor(o[e], 8, 64);
-      o[e] += __shfl_xor(o[e], 16, 64);
-      o[e] += __shfl_xor(o[e], 32, 64);
+      o[e] = xor8_sum(o[e]);
+      o[e] = xor16_sum(o[e]);
+      o[e] = xor32_sum(o[e]);
     }
     if (kg == 0) {
       const float inv = 1.f / lsum;
@@ -509,9 +509,9 @@ __global__ __launch_bounds__(64) void k_self_attn(const T* __restrict__ q, int l
   }
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
-    o[e] += __shfl_xor(o[e], 8, 64);
-    o[e] += __shfl_xor(o[e], 16, 64);
-    o[e] += __shfl_xor(o[e], 32, 64);
+    o[e] = xor8_sum(o[e]);
+    o[e] = xor16_sum(o[e]);
+    o[e] = xor32_sum(o[e]);
   }
   if (kg == 0) {
     const float inv = 1.f / sum;
@@ -652,9 +652,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void
     }
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
-      o[e] += __shfl_xor(o[e], 8, 64);
-      o[e] += __shfl_xor(o[e], 16, 64);
-      o[e] += __shfl_xor(o[e], 32, 64);
+      o[e] = xor8_sum(o[e]);
+      o[e] = xor16_sum(o[e]);
+      o[e] = xor32_sum(o[e]);
     }
     if (kg == 0) {
       const float e_cur = __expf(s_cur - m), inv = 1.f / (lsum + e_cur);
@@ -730,9 +730,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void
   }
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
-    o[e] += __shfl_xor(o[e], 8, 64);
-    o[e] += __shfl_xor(o[e], 16, 64);
-    o[e] += __shfl_xor(o[e], 32, 64);
+    o[e] = xor8_sum(o[e]);
+    o[e] = xor16_sum(o[e]);
+    o[e] = xor32_sum(o[e]);
   }
   if (kg == 0) {
     const float inv = 1.f / sum;
@@ -913,9 +913,9 @@ __global__ __launch_bounds__(64 * SA_GMAX) void k_self_attn_grp(const float* __r
   }
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
-    o[e] += __shfl_xor(o[e], 8, 64);
-    o[e] += __shfl_xor(o[e], 16, 64);
-    o[e] += __shfl_xor(o[e], 32, 64);
+    o[e] = xor8_sum(o[e]);
+    o[e] = xor16_sum(o[e]);
+    o[e] = xor32_sum(o[e]);
   }
   if (kg == 0) {
     const float e_cur = __expf(s_cur - m), inv = 1.f / (lsum + e_cur);
@@ -1102,8 +1102,8 @@ __global__ __launch_bounds__(64 * NW) void k_cross_attn(const T* __restrict__ q,
           else if (qslot >= 0 && qvalid) qk_out[((int64_t)qslot * qk_rows + row0 + qr) * Tk + key] = sc[kt][j];
           mx = fmaxf(mx, sc[kt][j]);
         }
-      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      mx = xor16_max(mx);
+      mx = xor32_max(mx);
       m = mx;
       Frag<T> pf[2];
       float ps = 0.f;
@@ -1115,8 +1115,8 @@ __global__ __launch_bounds__(64 * NW) void k_cross_attn(const T* __restrict__ q,
           ps += p;
           pf[kt >> 1].v[(kt & 1) * 4 + j] = from_f32<T>(p);
         }
-      ps += __shfl_xor(ps, 16, 64);
-      ps += __shfl_xor(ps, 32, 64);
+      ps = xor16_sum(ps);
+      ps = xor32_sum(ps);
       l = ps;
 #pragma unroll
       for (int s = 0; s < 2; ++s)
@@ -1299,8 +1299,8 @@ __global__ __launch_bounds__(512, 1) void k_xattn_seg(const T* __restrict__ q, i
         if (kt0 + kt * 16 + 4 * g + j >= Tk) sc[kt][j] = -INFINITY;
         mx = fmaxf(mx, sc[kt][j]);
       }
-    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    mx = xor16_max(mx);
+    mx = xor32_max(mx);
     Frag<T> pf[2];
     float ps = 0.f;
 #pragma unroll
@@ -1311,8 +1311,8 @@ __global__ __launch_bounds__(512, 1) void k_xattn_seg(const T* __restrict__ q, i
         ps += pv;
         pf[kt >> 1].v[(kt & 1) * 4 + j] = from_f32<T>(pv);
       }
-    ps += __shfl_xor(ps, 16, 64);
-    ps += __shfl_xor(ps, 32, 64);
+    ps = xor16_sum(ps);
+    ps = xor32_sum(ps);
     float4_t acc[4];
 #pragma unroll
     for (int dt = 0; dt < 4; ++dt) acc[dt] = (float4_t){0.f, 0.f, 0.f, 0.f};
