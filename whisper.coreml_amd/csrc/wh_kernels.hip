@@ -761,7 +761,10 @@ WH_DEV void sa_glds16(const void* src, void* lds) {
 }
 
 constexpr int SA_GMAX = 8;
-template <typename T>
+// PK keys per pass: 128 (k_self_attn_qkv's passes, bit-identical) or 64 (half the register
+// buffers: at <= 168 VGPRs two 5-wave workgroups share a CU, so the 400 (window, head)
+// workgroups of 20 windows run in one round; its own passes, so its own bits)
+template <typename T, int PK>
 __global__ __launch_bounds__(64 * SA_GMAX) void k_self_attn_grp(const float* __restrict__ part, int nsplit,
                                                                  int64_t part_stride, const float* __restrict__ bqkv,
                                                                  int ns, T* __restrict__ kc, T* __restrict__ vc,
@@ -769,10 +772,13 @@ __global__ __launch_bounds__(64 * SA_GMAX) void k_self_attn_grp(const float* __r
                                                                  const int* __restrict__ anc, int G, int nbeam, int H,
                                                                  int ctx, T* __restrict__ out, int ldo) {
   static_assert(sizeof(T) == 2, "fp16 path");
-  __shared__ __attribute__((aligned(1024))) T kref[128 * 64];
-  __shared__ __attribute__((aligned(1024))) T vref[128 * 64];
+  static_assert(PK == 128 || PK == 64, "keys per pass");
+  constexpr int NKI = PK / 8;  // glds instructions of 8 rows per K (and per V) stage
+  constexpr int VU = PK / 8;   // V rows per lane per pass
+  __shared__ __attribute__((aligned(1024))) T kref[PK * 64];
+  __shared__ __attribute__((aligned(1024))) T vref[PK * 64];
   __shared__ int slot_of[SA_GMAX][512];
-  __shared__ __attribute__((aligned(16))) float qs[SA_GMAX][64], vs[SA_GMAX][64], sc[SA_GMAX][128];
+  __shared__ __attribute__((aligned(16))) float qs[SA_GMAX][64], vs[SA_GMAX][64], sc[SA_GMAX][PK];
   const int lane = threadIdx.x & 63, sl = threadIdx.x >> 6;
   const int h = blockIdx.x % H, w = blockIdx.x / H, row = w * G + sl;
   const int* an = anc + ((int64_t)w * G + sl) * ctx;
@@ -830,14 +836,14 @@ __global__ __launch_bounds__(64 * SA_GMAX) void k_self_attn_grp(const float* __r
   float m = s_cur, lsum = 0.f, o[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) o[e] = 0.f;
-  for (int p0 = 0; p0 < pos; p0 += 128) {
-    // beam 0's rows p0 .. p0 + 127 (< pos) -> LDS: 16 K and 16 V instructions of 8 rows,
-    // dealt over the G waves; lane (row r0 + lane / 8, chunk lane % 8)
-    for (int i = sl; i < 32; i += G) {
-      const int r0 = (i & 15) * 8, r = r0 + (lane >> 3), p = p0 + r;
+  for (int p0 = 0; p0 < pos; p0 += PK) {
+    // beam 0's rows p0 .. p0 + PK - 1 (< pos) -> LDS: PK / 8 K and PK / 8 V instructions of
+    // 8 rows, dealt over the G waves; lane (row r0 + lane / 8, chunk lane % 8)
+    for (int i = sl; i < 2 * NKI; i += G) {
+      const int r0 = (i % NKI) * 8, r = r0 + (lane >> 3), p = p0 + r;
       if (p <= plast) {
         const int pc = lane & 7;
-        if (i < 16) {  // K: physical chunk pc holds logical chunk pc ^ ((r >> 1) & 7)
+        if (i < NKI) {  // K: physical chunk pc holds logical chunk pc ^ ((r >> 1) & 7)
           sa_glds16(kc + kv_off(slot_of[0][p], p) + 8 * (pc ^ ((r >> 1) & 7)), kref + r0 * 64);
         } else {
           sa_glds16(vc + kv_off(slot_of[0][p], p) + 8 * pc, vref + r0 * 64);
@@ -847,19 +853,21 @@ __global__ __launch_bounds__(64 * SA_GMAX) void k_self_attn_grp(const float* __r
     // this beam's own rows at or past d, straight from HBM into registers
     const int pa = min(p0 + lane, plast), pb = min(p0 + 64 + lane, plast);
     const bool la = pa < d, lb = pb < d;
-    Frag<T> ka[8], kb[8], vf[16];
+    Frag<T> ka[8], kb[PK == 128 ? 8 : 1], vf[VU];
     if (!la) {
       const T* ra = kc + kv_off(slot_of[sl][pa], pa);
 #pragma unroll
       for (int c = 0; c < 8; ++c) frag_load(ka[c], ra + 8 * c);
     }
-    if (!lb) {
-      const T* rb = kc + kv_off(slot_of[sl][pb], pb);
+    if constexpr (PK == 128) {
+      if (!lb) {
+        const T* rb = kc + kv_off(slot_of[sl][pb], pb);
 #pragma unroll
-      for (int c = 0; c < 8; ++c) frag_load(kb[c], rb + 8 * c);
+        for (int c = 0; c < 8; ++c) frag_load(kb[c], rb + 8 * c);
+      }
     }
 #pragma unroll
-    for (int u = 0; u < 16; ++u) {
+    for (int u = 0; u < VU; ++u) {
       const int pc = min(p0 + kg + 8 * u, plast);
       if (pc >= d) frag_load(vf[u], vc + kv_off(slot_of[sl][pc], pc) + dc);
     }
@@ -870,13 +878,15 @@ __global__ __launch_bounds__(64 * SA_GMAX) void k_self_attn_grp(const float* __r
 #pragma unroll
       for (int c = 0; c < 8; ++c) ka[c].v = *reinterpret_cast<const half8_t*>(kref + r * 64 + 8 * (c ^ sw));
     }
-    if (lb) {
-      const int r = pb - p0, sw = (r >> 1) & 7;
+    if constexpr (PK == 128) {
+      if (lb) {
+        const int r = pb - p0, sw = (r >> 1) & 7;
 #pragma unroll
-      for (int c = 0; c < 8; ++c) kb[c].v = *reinterpret_cast<const half8_t*>(kref + r * 64 + 8 * (c ^ sw));
+        for (int c = 0; c < 8; ++c) kb[c].v = *reinterpret_cast<const half8_t*>(kref + r * 64 + 8 * (c ^ sw));
+      }
     }
 #pragma unroll
-    for (int u = 0; u < 16; ++u) {
+    for (int u = 0; u < VU; ++u) {
       const int pc = min(p0 + kg + 8 * u, plast);
       if (pc < d) vf[u].v = *reinterpret_cast<const half8_t*>(vref + (pc - p0) * 64 + dc);
     }
@@ -889,22 +899,22 @@ __global__ __launch_bounds__(64 * SA_GMAX) void k_self_attn_grp(const float* __r
       for (int e = 0; e < 8; ++e) {
         const float qe = e < 4 ? q0[e] : q1[e - 4];
         sa += qe * to_f32(ka[c].v[e]);
-        sb += qe * to_f32(kb[c].v[e]);
+        if constexpr (PK == 128) sb += qe * to_f32(kb[c].v[e]);
       }
     }
-    const bool va = p0 + lane < pos, vb = p0 + 64 + lane < pos;
+    const bool va = p0 + lane < pos, vb = PK == 128 && p0 + 64 + lane < pos;
     const float mp = wave_max(fmaxf(va ? sa : -INFINITY, vb ? sb : -INFINITY));
     const float mn = fmaxf(m, mp), scale = __expf(m - mn);
     m = mn;
     const float ea = va ? __expf(sa - m) : 0.f, eb = vb ? __expf(sb - m) : 0.f;
     lsum = lsum * scale + wave_sum(ea + eb);
     sc[sl][lane] = ea;
-    sc[sl][64 + lane] = eb;
+    if constexpr (PK == 128) sc[sl][64 + lane] = eb;
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #pragma unroll
     for (int e = 0; e < 8; ++e) o[e] *= scale;
 #pragma unroll
-    for (int u = 0; u < 16; ++u) {
+    for (int u = 0; u < VU; ++u) {
       const float pw = sc[sl][kg + 8 * u];  // 0 past the end
 #pragma unroll
       for (int e = 0; e < 8; ++e) o[e] += pw * to_f32(vf[u].v[e]);
@@ -939,15 +949,22 @@ int launch_self_attn_qkv(const float* part, int nsplit, int64_t part_stride, con
   // fp16 beams, tuning build only (WHISPER_HIP_SA_GRP=1): the grouped form, same arithmetic
   // per row.  Measured slower at every context length (20 windows: step 3.456 -> 3.655 ms
   // at 12 tokens, 3.834 -> 4.114 at 220, profiles/r04/self_attn_grp_ab.txt): at 238 VGPRs a
-  // CU holds one 5-wave workgroup, so the 400 (window, head) workgroups run in two rounds
-  static const bool grp = [] {
+  // CU holds one 5-wave workgroup, so the 400 (window, head) workgroups run in two rounds.
+  // WHISPER_HIP_SA_GRP=2: 64-key passes, 132 VGPRs, one round — slower still (3.423 -> 3.523
+  // ms at 12 tokens, 3.819 -> 4.145 at 220, profiles/r04/self_attn_grp64_ab.txt): the
+  // growth with the context is the passes' round trips, not the bytes the beams share
+  static const int grp = [] {
     const char* e = tune_env("WHISPER_HIP_SA_GRP");
-    return e && e[0] == '1';
+    return e ? atoi(e) : 0;
   }();
   if constexpr (sizeof(T) == 2) {
     if (grp && anc_beams >= 2 && anc_beams <= SA_GMAX && ctx <= 512) {
-      k_self_attn_grp<T><<<(rows / anc_beams) * H, 64 * anc_beams, 0, st>>>(part, nsplit, part_stride, bqkv, ns, kc, vc,
-                                                                            rp, anc, anc_beams, nbeam, H, ctx, out, ldo);
+      if (grp == 2)
+        k_self_attn_grp<T, 64><<<(rows / anc_beams) * H, 64 * anc_beams, 0, st>>>(
+            part, nsplit, part_stride, bqkv, ns, kc, vc, rp, anc, anc_beams, nbeam, H, ctx, out, ldo);
+      else
+        k_self_attn_grp<T, 128><<<(rows / anc_beams) * H, 64 * anc_beams, 0, st>>>(
+            part, nsplit, part_stride, bqkv, ns, kc, vc, rp, anc, anc_beams, nbeam, H, ctx, out, ldo);
       return 0;
     }
   }
