@@ -359,7 +359,9 @@ void launch_attn_enc(const T* qkv, int ld, int ns, int H, int Tlen, int nwin, in
 // One wave per (row, head).  Keys = positions 0..pos of the row's sequence; position
 // p < pos lives in beam slot anc[win][slot][p] (beam reorder by index indirection,
 // no KV copies), position pos in the row's own slot.  Cache: [win][slot][head][ctx][64].
-template <typename T>
+// PIPE (fp16, round 4): 64-key passes with the next pass's loads in flight, as
+// k_self_attn_qkv<T, true>
+template <typename T, bool PIPE = false>
 __global__ __launch_bounds__(64) void k_self_attn(const T* __restrict__ q, int ldq, const T* __restrict__ kc,
                                                   const T* __restrict__ vc, const int* __restrict__ row_win,
                                                   const int* __restrict__ row_slot, const int* __restrict__ row_pos,
@@ -382,6 +384,78 @@ __global__ __launch_bounds__(64) void k_self_attn(const T* __restrict__ q, int l
   const int64_t head_stride = (int64_t)ctx * 64;
   const int64_t wbase = (int64_t)w * nbeam;
   auto kv_off = [&](int slot, int p) -> int64_t { return ((wbase + slot) * H + h) * head_stride + (int64_t)p * 64; };
+  if constexpr (sizeof(T) == 2 && PIPE) {
+    int sv[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) sv[i] = an[min(lane + 64 * i, ctx - 1)];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int pp = lane + 64 * i;
+      if (pp <= pos) slot_of[pp] = pp == pos ? sl : sv[i];
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // one wave: its own LDS writes
+    const int kg = lane >> 3, dc = (lane & 7) * 8;
+    float m = -INFINITY, lsum = 0.f, o[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] = 0.f;
+    auto load = [&](int p0, Frag<T>(&k)[8], Frag<T>(&v)[8]) {
+      const int pa = min(p0 + lane, pos);
+      const T* ra = kc + kv_off(slot_of[pa], pa);
+#pragma unroll
+      for (int c = 0; c < 8; ++c) frag_load(k[c], ra + 8 * c);
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int pc = min(p0 + kg + 8 * u, pos);
+        frag_load(v[u], vc + kv_off(slot_of[pc], pc) + dc);
+      }
+    };
+    auto pass = [&](int p0, const Frag<T>(&k)[8], const Frag<T>(&v)[8]) {
+      float sa = 0.f;
+#pragma unroll
+      for (int c = 0; c < 8; ++c)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) sa += qv[8 * c + e] * to_f32(k[c].v[e]);
+      const bool va = p0 + lane <= pos;
+      const float mp = wave_max(va ? sa : -INFINITY);
+      const float mn = fmaxf(m, mp), scale = __expf(m - mn);
+      m = mn;
+      const float ea = va ? __expf(sa - m) : 0.f;
+      lsum = lsum * scale + wave_sum(ea);
+      sc[lane] = ea;
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o[e] *= scale;
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const float pw = sc[kg + 8 * u];  // 0 past the end
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o[e] += pw * to_f32(v[u].v[e]);
+      }
+    };
+    Frag<T> ka[8], va[8], kb[8], vb[8];
+    load(0, ka, va);
+    int p0 = 0;
+    for (; p0 + 64 <= pos; p0 += 128) {
+      load(p0 + 64, kb, vb);
+      pass(p0, ka, va);
+      if (p0 + 128 <= pos) load(p0 + 128, ka, va);
+      pass(p0 + 64, kb, vb);
+    }
+    if (p0 <= pos) pass(p0, ka, va);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      o[e] = xor8_sum(o[e]);
+      o[e] = xor16_sum(o[e]);
+      o[e] = xor32_sum(o[e]);
+    }
+    if (kg == 0) {
+      const float inv = 1.f / lsum;
+      T* op = out + (int64_t)row * ldo + h * 64 + dc;
+      store4(op, o[0] * inv, o[1] * inv, o[2] * inv, o[3] * inv);
+      store4(op + 4, o[4] * inv, o[5] * inv, o[6] * inv, o[7] * inv);
+    }
+    return;
+  }
   if constexpr (sizeof(T) == 2) {
     // round 3 (fp16): the k_self_attn_qkv schedule — the ancestry of every context
     // position in the first round trip (8 per lane, with q), then per 128-key pass K
@@ -526,6 +600,19 @@ void launch_self_attn(const T* q, int ldq, const T* kc, const T* vc, const int* 
                       const int* anc, int anc_beams, int nbeam, int H, int ctx, T* out, int ldo, int rows,
                       hipStream_t st) {
   if (rows <= 0) return;
+  // tuning build only (WHISPER_HIP_SA_PIPE1=1): the pipelined 64-key passes at one window
+  // measured p50 1.670 -> 1.679 ms per token (profiles/r04/self_attn_pipe_ab.txt): not kept
+  static const bool pipe = [] {
+    const char* e = tune_env("WHISPER_HIP_SA_PIPE1");
+    return e && e[0] == '1';
+  }();
+  if constexpr (sizeof(T) == 2) {
+    if (pipe) {
+      k_self_attn<T, true><<<dim3(rows, H), 64, 0, st>>>(q, ldq, kc, vc, rw, rs, rp, anc, anc_beams, nbeam, H, ctx, out,
+                                                         ldo);
+      return;
+    }
+  }
   k_self_attn<T><<<dim3(rows, H), 64, 0, st>>>(q, ldq, kc, vc, rw, rs, rp, anc, anc_beams, nbeam, H, ctx, out, ldo);
 }
 
@@ -539,7 +626,12 @@ void launch_self_attn(const T* q, int ldq, const T* kc, const T* vc, const int* 
 // beams of one (window, head), whose ancestries mostly name the same cached (slot,
 // position) rows, run on one XCD and share its L2 (x-fastest order put them on G
 // different XCDs).
-template <typename T>
+//
+// PIPE (fp16, round 4): passes of 64 keys, the NEXT pass's K and V loads issued before
+// the current pass is computed (two register buffers of 8 K + 8 V fragments), q read from
+// LDS: at long contexts the passes' round trips overlap instead of adding up (the step's
+// growth over the decode is those round trips, profiles/r04/self_attn_grp64_ab.txt).
+template <typename T, bool PIPE = false>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void k_self_attn_qkv(const float* __restrict__ part, int nsplit, int64_t part_stride,
                                                       const float* __restrict__ bqkv, int ns, T* __restrict__ kc,
                                                       T* __restrict__ vc, const int* __restrict__ row_win,
@@ -598,6 +690,74 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void
   // the block is one wave: its LDS writes are visible to all its lanes once they have
   // completed (no barrier, and no wait for the K/V row stores above)
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  if constexpr (sizeof(T) == 2 && PIPE) {
+    const int kg = lane >> 3, dc = (lane & 7) * 8;
+    float m = s_cur, lsum = 0.f, o[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] = 0.f;
+    auto load = [&](int p0, Frag<T>(&k)[8], Frag<T>(&v)[8]) {
+      const int pa = min(p0 + lane, plast);
+      const T* ra = kc + kv_off(slot_of[pa], pa);
+#pragma unroll
+      for (int c = 0; c < 8; ++c) frag_load(k[c], ra + 8 * c);
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int pc = min(p0 + kg + 8 * u, plast);
+        frag_load(v[u], vc + kv_off(slot_of[pc], pc) + dc);
+      }
+    };
+    auto pass = [&](int p0, const Frag<T>(&k)[8], const Frag<T>(&v)[8]) {
+      float sa = 0.f;
+#pragma unroll
+      for (int c = 0; c < 8; ++c) {
+        const float4_t q0 = *reinterpret_cast<const float4_t*>(&qs[8 * c]);
+        const float4_t q1 = *reinterpret_cast<const float4_t*>(&qs[8 * c + 4]);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) sa += (e < 4 ? q0[e] : q1[e - 4]) * to_f32(k[c].v[e]);
+      }
+      const bool va = p0 + lane < pos;
+      const float mp = wave_max(va ? sa : -INFINITY);
+      const float mn = fmaxf(m, mp), scale = __expf(m - mn);
+      m = mn;
+      const float ea = va ? __expf(sa - m) : 0.f;
+      lsum = lsum * scale + wave_sum(ea);
+      sc[lane] = ea;
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o[e] *= scale;
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const float pw = sc[kg + 8 * u];  // 0 past the end
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o[e] += pw * to_f32(v[u].v[e]);
+      }
+    };
+    Frag<T> ka[8], va[8], kb[8], vb[8];
+    if (pos > 0) load(0, ka, va);
+    int p0 = 0;
+    for (; p0 + 64 < pos; p0 += 128) {
+      load(p0 + 64, kb, vb);
+      pass(p0, ka, va);
+      if (p0 + 128 < pos) load(p0 + 128, ka, va);
+      pass(p0 + 64, kb, vb);
+    }
+    if (p0 < pos) pass(p0, ka, va);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      o[e] = xor8_sum(o[e]);
+      o[e] = xor16_sum(o[e]);
+      o[e] = xor32_sum(o[e]);
+    }
+    if (kg == 0) {
+      const float e_cur = __expf(s_cur - m), inv = 1.f / (lsum + e_cur);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o[e] = (o[e] + e_cur * vs[dc + e]) * inv;
+      T* op = out + (int64_t)row * ldo + h * 64 + dc;
+      store4(op, o[0], o[1], o[2], o[3]);
+      store4(op + 4, o[4], o[5], o[6], o[7]);
+    }
+    return;
+  }
   float qv[64];
 #pragma unroll
   for (int c = 0; c < 64; ++c) qv[c] = qs[c];
@@ -965,6 +1125,20 @@ int launch_self_attn_qkv(const float* part, int nsplit, int64_t part_stride, con
       else
         k_self_attn_grp<T, 128><<<(rows / anc_beams) * H, 64 * anc_beams, 0, st>>>(
             part, nsplit, part_stride, bqkv, ns, kc, vc, rp, anc, anc_beams, nbeam, H, ctx, out, ldo);
+      return 0;
+    }
+  }
+  // fp16: the pipelined 64-key passes (WHISPER_HIP_SA_PIPE=0 in the tuning build: the
+  // 128-key passes): 20-window step 3.419 -> 3.363 ms at 12 tokens, 3.810 -> 3.756 at 220,
+  // config 3 675.6 -> 684.6 xRT (profiles/r04/self_attn_pipe_ab.txt)
+  static const bool pipe = [] {
+    const char* e = tune_env("WHISPER_HIP_SA_PIPE");
+    return !(e && e[0] == '0');
+  }();
+  if constexpr (sizeof(T) == 2) {
+    if (pipe) {
+      k_self_attn_qkv<T, true><<<rows * H, 64, 0, st>>>(part, nsplit, part_stride, bqkv, ns, kc, vc, rw, rs, rp, anc,
+                                                       anc_beams, nbeam, H, ctx, out, ldo);
       return 0;
     }
   }
