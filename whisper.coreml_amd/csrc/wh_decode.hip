@@ -325,12 +325,25 @@ template <typename T, int NT>
 __device__ void merge_embed_rows(const MergeEmbed& em, int w, int G, int pos, const int* newtok, int tid) {
   const T* E = reinterpret_cast<const T*>(em.E);
   const T* P = reinterpret_cast<const T*>(em.P);
-  const int n4 = em.n / 4;
-  for (int i = tid; i < G * n4; i += NT) {
-    const int b = i / n4, c = 4 * (i - b * n4), r = w * G + b;
-    const float4_t e = load4f(E + (int64_t)newtok[b] * em.n + c), p = load4f(P + (int64_t)pos * em.n + c);
-    const float4_t v = e + p;
-    store4(em.x + (int64_t)r * em.n + c, v[0], v[1], v[2], v[3]);
+  const int n4 = em.n / 4, total = G * n4;
+  constexpr int EB = 4;  // loads of EB items issued before their stores (one round trip per batch)
+  for (int i0 = 0; i0 < total; i0 += NT * EB) {
+    float4_t e[EB], p[EB];
+#pragma unroll
+    for (int u = 0; u < EB; ++u) {
+      const int i = min(i0 + tid + NT * u, total - 1), b = i / n4, c = 4 * (i - b * n4);
+      e[u] = load4f(E + (int64_t)newtok[b] * em.n + c);
+      p[u] = load4f(P + (int64_t)pos * em.n + c);
+    }
+#pragma unroll
+    for (int u = 0; u < EB; ++u) {
+      const int i = i0 + tid + NT * u;
+      if (i < total) {
+        const int b = i / n4, c = 4 * (i - b * n4), r = w * G + b;
+        const float4_t v = e[u] + p[u];
+        store4(em.x + (int64_t)r * em.n + c, v[0], v[1], v[2], v[3]);
+      }
+    }
   }
   if (tid < G) em.row_pos[w * G + tid] = pos;
 }

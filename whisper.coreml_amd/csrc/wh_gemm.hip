@@ -563,15 +563,28 @@ __global__ __launch_bounds__(512) void k_vocab_small(GemmArgs a) {
         }
     }
   } else {  // stage the group's X rows (rows >= M: zeros)
+    // in batches of SB chunks per thread, every load of a batch before its LDS writes
     const int cpr = K * (int)sizeof(T) / 16, total = RG * cpr;
-    for (int c = tid; c < total; c += 512) {
-      const int row = c / cpr, col = c - row * cpr;
-      float4_t v = (float4_t){0.f, 0.f, 0.f, 0.f};
-      if (m0 + row < a.M) {
-        const int xr = a.x_rows ? a.x_rows[m0 + row] : m0 + row;
-        v = *reinterpret_cast<const float4_t*>(reinterpret_cast<const char*>(X + (int64_t)xr * a.ldx) + col * 16);
+    constexpr int SB = 5;
+    for (int c0 = 0; c0 < total; c0 += 512 * SB) {
+      float4_t v[SB];
+#pragma unroll
+      for (int u = 0; u < SB; ++u) {
+        const int c = min(c0 + tid + 512 * u, total - 1), row = c / cpr, col = c - row * cpr;
+        v[u] = (float4_t){0.f, 0.f, 0.f, 0.f};
+        if (m0 + row < a.M) {
+          const int xr = a.x_rows ? a.x_rows[m0 + row] : m0 + row;
+          v[u] = *reinterpret_cast<const float4_t*>(reinterpret_cast<const char*>(X + (int64_t)xr * a.ldx) + col * 16);
+        }
       }
-      *reinterpret_cast<float4_t*>(xsv + row * xrow + col * 16) = v;
+#pragma unroll
+      for (int u = 0; u < SB; ++u) {
+        const int c = c0 + tid + 512 * u;
+        if (c < total) {
+          const int row = c / cpr, col = c - row * cpr;
+          *reinterpret_cast<float4_t*>(xsv + row * xrow + col * 16) = v[u];
+        }
+      }
     }
   }
   __syncthreads();
