@@ -27,9 +27,16 @@ constexpr int TBM = 128, TBN = 128, TKB = 128;  // TKB = bytes of K per tile row
 constexpr int TROW = TKB + 16;                  // padded LDS row stride (bytes): conflict-free b128 reads
 
 // TBN_ = 128 or 64 output columns per tile (64: grids below one tile per CU, e.g. the
-// n-wide encoder GEMMs of a single window: 120 -> 240 workgroups)
-template <typename T, int EPI, int TBN_ = TBN>
+// n-wide encoder GEMMs of a single window: 120 -> 240 workgroups).
+// KZ = 2 (round 4, the single-window encoder's residual GEMMs): each tile's K is split in
+// two halves run by two workgroups (480 for 240 tiles: two per CU), which meet per wave in
+// the launch: each wave stores its fp32 sub-tile write-through (sc1) into a.p1_slab,
+// drains it, adds to the (tile, wave) counter (relaxed agent atomic); the second arriver
+// re-arms the counter, loads the other half with sc1 loads and adds: acc + other, which is
+// the same bits whichever half arrives last (fp32 addition commutes), then the epilogue.
+template <typename T, int EPI, int TBN_ = TBN, int KZ = 1>
 __global__ __launch_bounds__(256, 2) void k_gemm_tile(GemmArgs a) {
+  static_assert(KZ == 1 || KZ == 2, "two K halves at most (their sum commutes)");
   constexpr int BK = TKB / (int)sizeof(T);  // 64 half / 32 float
   constexpr int KS = BK / 32;               // k-steps per tile
   constexpr int WCH = TBN_ / 32;            // W chunks per thread (TBN_ rows x 8 chunks / 256)
@@ -38,7 +45,9 @@ __global__ __launch_bounds__(256, 2) void k_gemm_tile(GemmArgs a) {
 
   const int ntn = a.N / TBN_;
   const int ntm = (a.M + TBM - 1) / TBM;
-  const int bid = xcd_remap(blockIdx.x, ntm * ntn);
+  // the KZ halves of a tile are neighbours in the remapped order (same XCD)
+  const int rid = xcd_remap(blockIdx.x, ntm * ntn * KZ);
+  const int bid = rid / KZ, kz = rid - bid * KZ;
   const int tm = bid / ntn, tn = bid % ntn;
   const int m0 = tm * TBM, n0 = tn * TBN_;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -59,8 +68,9 @@ __global__ __launch_bounds__(256, 2) void k_gemm_tile(GemmArgs a) {
     int m = m0 + row;
     if (m >= a.M) m = a.M - 1;
     const int gi = m / a.x_group_rows, ri = m - gi * a.x_group_rows;
-    xsrc[i] = reinterpret_cast<const char*>(X + (int64_t)gi * a.x_group_stride + (int64_t)ri * a.ldx) + col * 16;
-    if (i < WCH) wsrc[i] = reinterpret_cast<const char*>(W + (int64_t)(n0 + row) * a.K) + col * 16;
+    const int64_t k0 = (int64_t)kz * (a.K / KZ);  // this workgroup's K half
+    xsrc[i] = reinterpret_cast<const char*>(X + (int64_t)gi * a.x_group_stride + (int64_t)ri * a.ldx + k0) + col * 16;
+    if (i < WCH) wsrc[i] = reinterpret_cast<const char*>(W + (int64_t)(n0 + row) * a.K + k0) + col * 16;
     lds_off[i] = row * TROW + col * 16;
   }
   // two register sets: the global loads of tile kt+2 are in flight while tile kt is
@@ -110,7 +120,7 @@ __global__ __launch_bounds__(256, 2) void k_gemm_tile(GemmArgs a) {
     }
   };
 
-  const int nk = a.K / BK;
+  const int nk = a.K / BK / KZ;
   gload(0, ra);
   gload(min(1, nk - 1), rb);
   sstore(0, ra);
@@ -127,6 +137,34 @@ __global__ __launch_bounds__(256, 2) void k_gemm_tile(GemmArgs a) {
     compute(1);
     if (kt + 2 < nk) sstore(0, ra);
     lds_barrier();
+  }
+
+  if constexpr (KZ > 1) {
+    constexpr int NE = 4 * NI;  // float4 per lane of the wave's 64 x TBN_/2 sub-tile
+    const int slot = bid * 4 + wave, nslot = ntm * ntn * 4;
+    const auto rs = wt_rsrc(a.p1_slab);
+    auto off = [&](int z, int e) { return (((z * nslot + slot) * NE + e) * 64 + lane) * 16; };
+#pragma unroll
+    for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < NI; ++ni) wt_store4(rs, off(kz, mi * NI + ni), acc[mi][ni]);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    int ticket = 0;
+    if (lane == 0) ticket = __hip_atomic_fetch_add(a.p1_cnt + slot, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    ticket = __shfl(ticket, 0, 64);
+    if (ticket != KZ - 1) return;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // no instruction: keeps the loads below the add
+    if (lane == 0) __hip_atomic_store(a.p1_cnt + slot, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    float4_t pv[4][NI];  // every load issued before the first add
+#pragma unroll
+    for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < NI; ++ni)
+        pv[mi][ni] = __builtin_bit_cast(float4_t, __builtin_amdgcn_raw_buffer_load_b128(rs, off(1 - kz, mi * NI + ni), 0, 16));
+#pragma unroll
+    for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < NI; ++ni) acc[mi][ni] += pv[mi][ni];
   }
 
   // epilogue: lane holds Y[m = m0+wr*64+mi*16+r][n = n0+wc*TBN_/2+ni*16+4g .. +3]
@@ -1009,6 +1047,15 @@ int launch_gemm_tiles(const GemmArgs& a, int epi, int tile_sel, hipStream_t st) 
     // n-wide encoder GEMMs: 120 -> 240 workgroups)
     const bool half = ntm * (a.N / TBN) < 256 && (a.N % 64) == 0 && tile_sel != 129;
     const int nwg = ntm * (a.N / (half ? 64 : TBN));
+    // two K halves per 128 x 64 tile where the caller hands over slabs + counters (the
+    // single-window encoder's residual GEMMs: out, fc2, conv2); p1_slabs in KB, 64 per tile
+    const bool kz2 = half && sizeof(T) == 2 && (epi == EPI_RESID || epi == EPI_GELU_POS) && a.p1_slab && a.p1_cnt &&
+                     (a.K / (TKB / (int)sizeof(T))) % 2 == 0 && (int64_t)nwg * 64 <= a.p1_slabs && tile_sel != 128;
+    if (kz2) {
+      if (epi == EPI_RESID) k_gemm_tile<T, EPI_RESID, 64, 2><<<2 * nwg, 256, 0, st>>>(a);
+      else k_gemm_tile<T, EPI_GELU_POS, 64, 2><<<2 * nwg, 256, 0, st>>>(a);
+      return 0;
+    }
     switch (epi) {
 #define CASE(E)                                                       \
   case E:                                                             \

@@ -60,6 +60,8 @@ constexpr int PRE_ROWS = 1024;    // min prefill rows per pass (the context size
 constexpr int MROWS = 3008;       // melT rows per window (1 pad + 3000 + slack for padded conv1 K)
 constexpr int H1ROWS = 3002;      // conv1 output rows per window (zero rows 0 and 3001)
 constexpr int KC = 9;
+// 128 x 64 tiles of a single window's n-wide encoder GEMMs (1500 rows: 12 row tiles)
+constexpr int EKZ_TILES(int n) { return 12 * (n / 64); }
 constexpr int RSPLIT = 16;      // max split-K slabs of the residual projections (decode rows <= 128)
 
 struct Arena {
@@ -192,6 +194,11 @@ struct Ctx : public wh_ctx {
   float* vs_rec = nullptr;   // k_vocab_sel records
   int* vs_cnt = nullptr;     // and its arrival counter (zero between launches)
   int* p1_cnt = nullptr;     // and arrival counters [4n/16] (zero between launches)
+  // single-window encoder: the residual GEMMs' K halves (k_gemm_tile KZ = 2) meet through
+  // these fp32 slabs (64 KB per 128 x 64 tile, 12 x n/64 tiles at 1500 rows) and
+  // per-(tile, wave) arrival counters (zero between launches)
+  float* ekz_slab = nullptr;
+  int* ekz_cnt = nullptr;
   float* xs_rec = nullptr;   // step cross-attention segment records [pair][XS_NSP][XREC]
   float* x2_d = nullptr;     // k_proj1 path: second residual buffer (deferred residual ping-pong)
   int* xs_cnt = nullptr;     // and (window, head) arrival counters
@@ -354,6 +361,7 @@ struct Ctx : public wh_ctx {
     addA((size_t)P1_SLABS * 256 * 4); addA((size_t)(4 * n / 16) * 4);  // k_proj1 split-K slabs + counters
     addA((size_t)Wcap * nh * XS_NSP * XREC * 4); addA((size_t)Wcap * nh * 4);  // cross-attention segment records
     addA((size_t)8 * n * 4);  // k_proj1 path (<= 8 rows, wh_proj.h P1_RMAX): the second residual buffer
+    addA((size_t)EKZ_TILES(n) * 65536); addA((size_t)EKZ_TILES(n) * 4 * 4);  // single-window encoder K halves
     HIPCHK(hipMalloc(&abase, ab));
     HIPCHK(hipMemset(abase, 0, ab));
     aa.base = (char*)abase;
@@ -391,7 +399,9 @@ struct Ctx : public wh_ctx {
     p1_slab = fa((size_t)P1_SLABS * 256); p1_cnt = ia(4 * n / 16);  // zeroed with the arena
     xs_rec = fa((size_t)Wcap * nh * XS_NSP * XREC); xs_cnt = ia((size_t)Wcap * nh);
     x2_d = fa((size_t)8 * n);
-    if (!S.seed || !S.cand_idx || !S.lp_cnt || !S.lpw_cnt || !vs_cnt || !p1_cnt || !xs_cnt || !x2_d) return fail(-3, "activation arena overflow");
+    ekz_slab = fa((size_t)EKZ_TILES(n) * 16384); ekz_cnt = ia((size_t)EKZ_TILES(n) * 4);  // zeroed with the arena
+    if (!S.seed || !S.cand_idx || !S.lp_cnt || !S.lpw_cnt || !vs_cnt || !p1_cnt || !xs_cnt || !x2_d || !ekz_cnt)
+      return fail(-3, "activation arena overflow");
     S.nw = Wcap; S.G = 1; S.ctx = CTX; S.hctx = HCTX; S.maxc = 16;
     HIPCHK(hipMalloc(&d_gmax, 64));
     d_gmax_f = (float*)(d_gmax + 4);
@@ -631,9 +641,19 @@ struct Ctx : public wh_ctx {
   }
 
   // ------------------------------------------------------------ encoder
-  int encode_chunk(int s0, int we) {
+  // single: the encode is ONE window (its decode batch runs the single-window path too):
+  // the residual GEMMs (conv2, out, fc2) split K in two halves inside the launch — within
+  // the fp16 bound of the multi-window encoder, not bit-equal to it, as k_proj1 in the step
+  int encode_chunk(int s0, int we, bool single = false) {
     const int n = ns;
     GemmArgs g;
+    const bool kz = single && we == 1 && sizeof(T) == 2 && !(tune_env("WHISPER_HIP_ENC_KZ") && tune_env("WHISPER_HIP_ENC_KZ")[0] == '0');
+    auto kz_on = [&](GemmArgs& ga) {
+      if (!kz) return;
+      ga.p1_slab = ekz_slab;
+      ga.p1_cnt = ekz_cnt;
+      ga.p1_slabs = EKZ_TILES(n) * 64;
+    };
     // mel windows -> time-major (T), conv1 as overlapping-row GEMM (lda = n_mels)
     launch_mel_windows<T>(d_mel, mel_frames, nm, d_seeks + s0, d_segs + s0, melT, (int64_t)MROWS * nm, MROWS, we, st);
     g = GemmArgs();
@@ -645,6 +665,7 @@ struct Ctx : public wh_ctx {
     g = GemmArgs();
     g.x_group_rows = 1500; g.x_group_stride = (int64_t)H1ROWS * n;
     g.out_f32 = x_e; g.ldo = n; g.pos = pos_enc;
+    kz_on(g);
     TRY(gemm(h1, 2 * n, conv2_w, conv2_b, we * 1500, n, 3 * n, EPI_GELU_POS, g));
     const int M = we * 1500;
     for (int l = 0; l < La; ++l) {
@@ -657,11 +678,13 @@ struct Ctx : public wh_ctx {
       TRY(gemm(xn_e, n, e.wqkv, e.bqkv, M, 3 * n, n, EPI_QKV_ENC, g));
       launch_attn_enc<T>(qkv_e, 3 * n, n, nh, 1500, we, (int64_t)1500 * 3 * n, vt_e, TKP, att_e, (int64_t)1500 * n, st);
       g = GemmArgs(); g.out_f32 = x_e; g.ldo = n;
+      kz_on(g);
       TRY(gemm(att_e, n, e.wo, e.bo, M, n, n, EPI_RESID, g));
       launch_layernorm<T>(x_e, xn_e, e.ln2_g, e.ln2_b, M, n, 1e-7f, nullptr, st);
       g = GemmArgs(); g.out = hm_e; g.ldo = 4 * n;
       TRY(gemm(xn_e, n, e.w1, e.b1, M, 4 * n, n, EPI_STORE_GELU, g));
       g = GemmArgs(); g.out_f32 = x_e; g.ldo = n;
+      kz_on(g);
       TRY(gemm(hm_e, 4 * n, e.w2, e.b2, M, n, 4 * n, EPI_RESID, g));
     }
     T* xa_s = xa + (size_t)s0 * 1500 * n;
@@ -689,7 +712,7 @@ struct Ctx : public wh_ctx {
     HIPCHK(hipMemcpyAsync(d_seeks, h_seeks.data(), n_win * 8, hipMemcpyHostToDevice, st));
     HIPCHK(hipMemcpyAsync(d_segs, segs, n_win * 4, hipMemcpyHostToDevice, st));
     const int WE = std::min(Wcap, enc_chunk());
-    for (int s0 = 0; s0 < n_win; s0 += WE) TRY(encode_chunk(s0, std::min(WE, n_win - s0)));
+    for (int s0 = 0; s0 < n_win; s0 += WE) TRY(encode_chunk(s0, std::min(WE, n_win - s0), n_win == 1));
     hipEventRecord(tm.b, st);
     HIPCHK(hipStreamSynchronize(st));
     float ms = 0;
@@ -1638,7 +1661,7 @@ struct Ctx : public wh_ctx {
       hipEventRecord(tm.b, st);
     } else if (what == 1) {
       hipEventRecord(tm.a, st);
-      for (int i = 0; i < iters; ++i) TRY(encode_chunk(0, 1));
+      for (int i = 0; i < iters; ++i) TRY(encode_chunk(0, 1, true));
       hipEventRecord(tm.b, st);
     } else if (what == 2 || what == 3 || what == 5 || what == 6) {
       // per-launch time of one decoder-step kernel at the current batch, over all
