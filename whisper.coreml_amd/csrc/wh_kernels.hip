@@ -1433,6 +1433,21 @@ WH_DEV float4_t xs_merge(int n, Get get) {
   return acc * inv;
 }
 
+#if WH_TUNING
+// tuning build: per-workgroup wall-clock marks (s_memrealtime, 100 MHz) of the last
+// k_xattn_seg launch, read by wh_tune_xs_trace (profiles/xattn_trace.py)
+constexpr int XS_MARKS = 8;
+__device__ unsigned long long g_xs_trace[256][XS_MARKS];
+#define XS_MARK(k)                                                                         \
+  do {                                                                                     \
+    if (threadIdx.x == 0) g_xs_trace[blockIdx.x][k] = __builtin_amdgcn_s_memrealtime();   \
+  } while (0)
+#else
+#define XS_MARK(k) \
+  do {             \
+  } while (0)
+#endif
+
 template <typename T, int QZ, int RR, typename S = float>
 __global__ __launch_bounds__(512, 1) void k_xattn_seg(const T* __restrict__ q, int ldq, const T* ck, const T* cvt, int Tk,
                                                      int H, int npair, int nsp, const int* __restrict__ win_row0,
@@ -1450,6 +1465,7 @@ __global__ __launch_bounds__(512, 1) void k_xattn_seg(const T* __restrict__ q, i
   const int nseg = npair * nsp, nwg = gridDim.x, b = blockIdx.x;
   const int s0 = (int)((int64_t)b * nseg / nwg), s1 = (int)((int64_t)(b + 1) * nseg / nwg), cnt = s1 - s0;
   const int pa = s0 / nsp, plast = (s1 - 1) / nsp;
+  XS_MARK(0);
 
   // local tile i: K and V fragments
   auto load_kv = [&](int i, Frag<T>(&kf)[4][2], Frag<T>(&vf)[4][2]) {
@@ -1549,6 +1565,7 @@ __global__ __launch_bounds__(512, 1) void k_xattn_seg(const T* __restrict__ q, i
     store4(&qs[j][t >> 4][(t & 15) * 4], qv[0], qv[1], qv[2], qv[3]);
   }
   asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // LDS only
+  XS_MARK(1);
 
   if (wave < cnt) {
     int i = wave;
@@ -1567,7 +1584,9 @@ __global__ __launch_bounds__(512, 1) void k_xattn_seg(const T* __restrict__ q, i
       tile(kA, vA, i);
     }
   }
+  XS_MARK(2);
   __syncthreads();
+  XS_MARK(3);
 
   // merge: RR * 16 threads per pair, (row qq, 4 columns dc)
   typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
@@ -1604,6 +1623,7 @@ __global__ __launch_bounds__(512, 1) void k_xattn_seg(const T* __restrict__ q, i
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its records
   __syncthreads();
+  XS_MARK(4);
   // the cut pairs: the first if it began before this range, the last if it continues
   // after it (the same pair when the range lies inside one pair)
   const bool cut_a = pa * nsp < s0 || pa * nsp + nsp > s1;
@@ -1614,6 +1634,7 @@ __global__ __launch_bounds__(512, 1) void k_xattn_seg(const T* __restrict__ q, i
     s_ticket[1] = cut_b && __hip_atomic_fetch_add(xq.split_cnt + plast, cb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + cb == nsp;
   }
   __syncthreads();
+  XS_MARK(5);
   if (part > 1 || !s_ticket[part]) return;
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // no instruction: keeps the loads below the add
   const int pj = part ? plast : pa;
@@ -1625,7 +1646,16 @@ __global__ __launch_bounds__(512, 1) void k_xattn_seg(const T* __restrict__ q, i
          l = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, rb + (1040 + qq) * 4, 0, 16));
          o = __builtin_bit_cast(float4_t, __builtin_amdgcn_raw_buffer_load_b128(rs, rb + (qq * 64 + dc) * 4, 0, 16));
        }));
+  XS_MARK(6);
 }
+
+#if WH_TUNING
+}  // namespace wh
+extern "C" int wh_tune_xs_trace(unsigned long long* out) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(wh::g_xs_trace), sizeof(wh::g_xs_trace)) == hipSuccess ? 0 : -1;
+}
+namespace wh {
+#endif
 
 // Workgroups for nseg = npair x nsp tiles (speed only; the numerics do not depend on it).
 //  * whole pairs per workgroup when that still fills >= 3/4 of the 256 CUs (20 windows:
