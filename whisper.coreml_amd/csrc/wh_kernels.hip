@@ -1448,7 +1448,7 @@ __device__ unsigned long long g_xs_trace[256][XS_MARKS];
   } while (0)
 #endif
 
-template <typename T, int QZ, int RR, typename S = float>
+template <typename T, int QZ, int RR, typename S = float, bool FULL = false>
 __global__ __launch_bounds__(512, 1) void k_xattn_seg(const T* __restrict__ q, int ldq, const T* ck, const T* cvt, int Tk,
                                                      int H, int npair, int nsp, const int* __restrict__ win_row0,
                                                      const int* __restrict__ win_nrows,
@@ -1469,7 +1469,10 @@ __global__ __launch_bounds__(512, 1) void k_xattn_seg(const T* __restrict__ q, i
 
   // local tile i: K and V fragments
   auto load_kv = [&](int i, Frag<T>(&kf)[4][2], Frag<T>(&vf)[4][2]) {
-    const int gs = s0 + i, p = gs / nsp, k = gs - p * nsp, wi = p / H, h = p - wi * H;
+    // i is wave-uniform: the tile's window slot comes by a scalar load (lgkmcnt).  Round 4:
+    // as a vector load it sat in vmcnt order, and the s_waitcnt vmcnt(0) before the K / V
+    // addresses drained the tile in flight: one tile per wave in flight, not two
+    const int gs = __builtin_amdgcn_readfirstlane(s0 + i), p = gs / nsp, k = gs - p * nsp, wi = p / H, h = p - wi * H;
     const int64_t off = (int64_t)win_slot[wi] * win_stride;
     const T* kbase = ck + off + (int64_t)h * TKP * 64;
     const T* vbase = cvt + off + (int64_t)h * 64 * TKP;
@@ -1540,30 +1543,62 @@ __global__ __launch_bounds__(512, 1) void k_xattn_seg(const T* __restrict__ q, i
   };
 
   Frag<T> kA[4][2], vA[4][2], kB[4][2], vB[4][2];
-  if (wave < cnt) load_kv(wave, kA, vA);
   // the query rows of the pairs this range touches -> LDS (rows past a window's beams
-  // repeat its last row; K / V stay in flight)
+  // repeat its last row).  Round 4: their loads are issued BEFORE the first tile's K / V:
+  // vmcnt retires loads in issue order, so the staging below waits for the query alone,
+  // the barrier passes ~a round trip in, and the second tile's K / V leave while the first
+  // burst is still landing (the query used to wait behind the whole first tile,
+  // profiles/xattn_trace.py: query staged at 5.3 us of a 34 us launch at 20 windows)
+  constexpr int NQP = XS_QP / 2;
+  // FULL (the launcher: every workgroup holds >= 8 tiles, one per wave at least): the order
+  // above; otherwise (few windows, <= 1 tile per wave) the first tile leaves first, as the
+  // query then has no second tile to overlap
+  if constexpr (!FULL) {
+    if (wave < cnt) load_kv(wave, kA, vA);
+  }
+  float4_t qld[NQP][QP ? QZ + 1 : 1];  // QP: the QZ slabs, then the bias
 #pragma unroll
-  for (int pass = 0; pass < XS_QP / 2; ++pass) {
+  for (int pass = 0; pass < NQP; ++pass) {
     const int j = 2 * pass + (tid >> 8), t = tid & 255;
-    const int pj = min(pa + j, plast), wj = pj / H, hj = pj - wj * H;
+    // wave-uniform pair: its window's metadata by scalar loads (lgkmcnt, not behind vmcnt)
+    const int pj = __builtin_amdgcn_readfirstlane(min(pa + j, plast)), wj = pj / H, hj = pj - wj * H;
     const int qq = min(t >> 4, win_nrows[wj] - 1), c = hj * 64 + (t & 15) * 4, row = win_row0[wj] + qq;
-    float4_t qv = (float4_t){0.f, 0.f, 0.f, 0.f};
     if constexpr (QP) {
-      float4_t pp[QP ? QZ : 1];
       const S* src = reinterpret_cast<const S*>(xq.part) + (int64_t)row * ldq + c;
 #pragma unroll
-      for (int z = 0; z < QZ; ++z) pp[z] = load4f(src + z * xq.stride);
-      qv = load4f(xq.bias + c);
-#pragma unroll
-      for (int z = 0; z < QZ; ++z) qv += pp[z];
+      for (int z = 0; z < QZ; ++z) qld[pass][z] = load4f(src + z * xq.stride);
+      qld[pass][QZ] = load4f(xq.bias + c);
     } else {
-      const T* src = q + (int64_t)row * ldq + c;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) qv[e] = (float)src[e];
+      qld[pass][0] = load4f(q + (int64_t)row * ldq + c);
     }
-    store4(&qs[j][t >> 4][(t & 15) * 4], qv[0], qv[1], qv[2], qv[3]);
   }
+  if constexpr (FULL) {
+    __builtin_amdgcn_sched_barrier(0);  // keep the K / V loads behind the query's
+    // every wave's query loads enter the CU's memory pipeline before any wave's K / V
+    // (a barrier that waits for nothing: no s_waitcnt before it)
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  auto stage_q = [&] {
+#pragma unroll
+    for (int pass = 0; pass < NQP; ++pass) {
+      const int j = 2 * pass + (tid >> 8), t = tid & 255;
+      float4_t qv = qld[pass][0];
+      if constexpr (QP) {
+        qv = qld[pass][QZ];
+#pragma unroll
+        for (int z = 0; z < QZ; ++z) qv += qld[pass][z];
+      }
+      store4(&qs[j][t >> 4][(t & 15) * 4], qv[0], qv[1], qv[2], qv[3]);
+    }
+  };
+  // FULL: unconditional (every wave has a tile), so no branch join: behind one the
+  // compiler's vmcnt bookkeeping made the query staging wait for the K / V loads as well
+  if constexpr (FULL) {
+    load_kv(wave, kA, vA);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  stage_q();
   asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // LDS only
   XS_MARK(1);
 
@@ -1699,13 +1734,22 @@ void launch_cross_attn(const T* q, int ldq, const T* ck, const T* cv, int Tk, in
   if (xq.max_rows >= 1 && xq.max_rows <= 16 && !qk_map && xq.split_rec && xq.split_cnt && nsp <= XS_NSP &&
       nwin * H <= xq.max_pairs) {
     const int npair = nwin * H;
-#define XS(QZ_, RR_)                                                                                              \
-  if (xq.part_half)                                                                                             \
-    k_xattn_seg<T, QZ_, RR_, half_t><<<xattn_seg_grid(npair, nsp, XsShape<RR_>::SMAX), 512, 0, st>>>(          \
-        q, ldq, ck, cv, Tk, H, npair, nsp, win_row0, win_nrows, win_slot, win_stride, xq, out, ldo);              \
+    // FULL: every workgroup's range holds >= 8 tiles (one per wave), e.g. 20 windows
+    const int nwg_xs = xattn_seg_grid(npair, nsp, xq.max_rows <= 8 ? XsShape<8>::SMAX : XsShape<16>::SMAX);
+    const bool full = (npair * nsp) / nwg_xs >= 8;
+#define XSF(QZ_, RR_, S_)                                                                                         \
+  if (full)                                                                                                     \
+    k_xattn_seg<T, QZ_, RR_, S_, true><<<nwg_xs, 512, 0, st>>>(q, ldq, ck, cv, Tk, H, npair, nsp, win_row0,       \
+                                                               win_nrows, win_slot, win_stride, xq, out, ldo);   \
   else                                                                                                          \
-    k_xattn_seg<T, QZ_, RR_><<<xattn_seg_grid(npair, nsp, XsShape<RR_>::SMAX), 512, 0, st>>>(                  \
-        q, ldq, ck, cv, Tk, H, npair, nsp, win_row0, win_nrows, win_slot, win_stride, xq, out, ldo)
+    k_xattn_seg<T, QZ_, RR_, S_, false><<<nwg_xs, 512, 0, st>>>(q, ldq, ck, cv, Tk, H, npair, nsp, win_row0,      \
+                                                                win_nrows, win_slot, win_stride, xq, out, ldo)
+#define XS(QZ_, RR_)          \
+  if (xq.part_half) {         \
+    XSF(QZ_, RR_, half_t);    \
+  } else {                    \
+    XSF(QZ_, RR_, float);     \
+  }
 #define XSR(QZ_)                        \
   if (xq.max_rows <= 8) {               \
     XS(QZ_, 8);                         \
@@ -1720,6 +1764,7 @@ void launch_cross_attn(const T* q, int ldq, const T* ck, const T* cv, int Tk, in
     }
 #undef XSR
 #undef XS
+#undef XSF
     return;
   }
   // first passes (prefill, alignment capture): one 64-key tile per wave, 8 waves per
