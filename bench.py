@@ -68,6 +68,11 @@ def parse():
     p.add_argument("--backend", default="nccl", help="torch.distributed backend of the ranks (nccl = RCCL)")
     p.add_argument("--launch-check", type=int, default=0,
                    help="only bring the ranks up, all-gather (rank, world) and print it from rank 0 (no GPU work)")
+    p.add_argument("--launch-check-fail-rank", type=int, default=-1,
+                   help="(launcher test) with --launch-check: this rank exits 3 after init while the others wait "
+                        "in a collective")
+    p.add_argument("--dist-timeout", type=float, default=900.0,
+                   help="seconds before a torch.distributed collective gives up")
     return p.parse_args()
 
 
@@ -79,24 +84,47 @@ def _free_port():
     return port
 
 
-def launch_ranks(args):
+def launch_ranks(args, poll_s=0.2, grace_s=10.0):
     """--gpus N without an external launcher: run this script as N rank processes.
 
     Called before anything in this process imports torch.cuda or the HIP library
-    (no exec: the children are new processes, this one only waits).  Returns the
-    exit code: 0 when every rank exited 0, else the first non-zero code."""
+    (no exec: the children are new processes, this one only waits).  The children are
+    polled together: the first one to exit non-zero ends the run — its siblings (which
+    may be blocked in a collective waiting for it) get SIGTERM, then SIGKILL after
+    ``grace_s`` — and its code is returned.  0 when every rank exited 0."""
     port = _free_port()
     procs = []
     for r in range(args.gpus):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(args.gpus), LOCAL_WORLD_SIZE=str(args.gpus),
                    MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
-    codes = [p.wait() for p in procs]
-    bad = [(r, c) for r, c in enumerate(codes) if c != 0]
-    if bad:
-        print(f"bench.py: rank(s) failed: {bad}", file=sys.stderr, flush=True)
-        return bad[0][1] if bad[0][1] > 0 else 1
-    return 0
+    failed = None  # (rank, code) of the first rank that failed
+    while failed is None and any(p.poll() is None for p in procs):
+        for r, p in enumerate(procs):
+            c = p.poll()
+            if c is not None and c != 0:
+                failed = (r, c)
+                break
+        else:
+            time.sleep(poll_s)
+    if failed is None:
+        failed = next(((r, p.returncode) for r, p in enumerate(procs) if p.returncode != 0), None)
+    if failed is None:
+        return 0
+    for p in procs:
+        if p.poll() is None:
+            p.terminate()
+    deadline = time.monotonic() + grace_s
+    for p in procs:
+        try:
+            p.wait(timeout=max(0.1, deadline - time.monotonic()))
+        except subprocess.TimeoutExpired:
+            p.kill()
+            p.wait()
+    print(f"bench.py: rank {failed[0]} failed with exit code {failed[1]}; "
+          f"rank(s) failed: {[(r, p.returncode) for r, p in enumerate(procs) if p.returncode != 0]}",
+          file=sys.stderr, flush=True)
+    return failed[1] if failed[1] > 0 else 1
 
 
 def dist_setup(args):
@@ -111,7 +139,10 @@ def dist_setup(args):
         if args.backend == "nccl":
             import torch
             torch.cuda.set_device(local)
-        dist.init_process_group(args.backend)
+        from datetime import timedelta
+        # bounded collectives: a rank that never arrives ends the run with an error
+        # instead of a hang (the launcher above also ends the survivors of a dead rank)
+        dist.init_process_group(args.backend, timeout=timedelta(seconds=args.dist_timeout))
         assert dist.get_world_size() == args.gpus
         pg = dist
     return world, rank, local, pg
@@ -121,6 +152,8 @@ def launch_check(args):
     """--launch-check 1: the ranks came up; rank 0 prints every rank's (rank, world)."""
     world, rank, _, pg = dist_setup(args)
     seen = [(rank, world)]
+    if pg is not None and rank == args.launch_check_fail_rank:
+        os._exit(3)  # dies after init; the other ranks block in the all-gather below
     if pg is not None:
         seen = [None] * world
         pg.all_gather_object(seen, (rank, pg.get_world_size()))
@@ -133,10 +166,8 @@ def launch_check(args):
 def allreduce_max(pg, x: float) -> float:
     if pg is None:
         return x
-    import torch
-    t = torch.tensor([x], dtype=torch.float32, device="cuda")
-    pg.all_reduce(t, op=pg.ReduceOp.MAX)
-    return float(t.item())
+    from whisper import distributed as D
+    return D.global_max(x)  # RCCL on a device tensor under nccl, a CPU tensor under gloo
 
 
 def barrier(pg):

@@ -51,3 +51,18 @@ def test_world_must_match_gpus():
              env_extra=dict(WORLD_SIZE="2", RANK="0", LOCAL_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT="29999"))
     assert p.returncode != 0
     assert "WORLD_SIZE 2" in p.stderr
+
+
+def test_launcher_ends_survivors_when_a_rank_dies_mid_collective():
+    # rank 1 exits 3 after init_process_group while rank 0 waits in an all-gather for it:
+    # the launcher must notice, terminate rank 0 and exit non-zero well inside 60 s
+    # (the collective's own timeout is set far beyond that, so only the launcher can end it)
+    import time
+    t0 = time.monotonic()
+    p = _run(["--gpus", "2", "--launch-check", "1", "--backend", "gloo", "--launch-check-fail-rank", "1",
+              "--dist-timeout", "600"], timeout=120)
+    dt = time.monotonic() - t0
+    assert p.returncode == 3, (p.returncode, p.stderr[-2000:])
+    assert "rank 1 failed with exit code 3" in p.stderr
+    assert dt < 60, dt
+    assert _json_lines(p.stdout) == []

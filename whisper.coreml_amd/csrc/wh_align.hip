@@ -243,8 +243,8 @@ int launch_dtw_jobs(const DtwJob* d_jobs, int n, int max_n, int in_lds, size_t l
   // one lane per row: the fewer waves, the cheaper each diagonal's barrier
   const int threads = dtw_threads(max_n);
   if (n <= 0) return 0;
-  if (in_lds) k_dtw<true><<<n, threads, lds, st>>>(d_jobs, sign);
-  else k_dtw<false><<<n, threads, lds, st>>>(d_jobs, sign);
+  if (in_lds) k_dtw<true><<<n, threads, lds, st>>>(d_jobs, sign), wh_launched("k_dtw");
+  else k_dtw<false><<<n, threads, lds, st>>>(d_jobs, sign), wh_launched("k_dtw");
   return 0;
 }
 
@@ -267,14 +267,14 @@ __global__ __launch_bounds__(256) void k_token_probs(const float* __restrict__ l
 
 void launch_align_matrix(float* qk, int64_t hs, int rows, int Tk, int F, int heads, int t0, int N, int width,
                          float* mat, hipStream_t st) {
-  k_align_softmax<<<dim3(rows, heads), 256, 0, st>>>(qk, hs, Tk, F);
-  k_align_znorm<<<dim3((F + 63) / 64, heads), 256, 0, st>>>(qk, hs, rows, Tk, F);
-  k_align_medmean<<<dim3((F + 255) / 256, N), 256, 0, st>>>(qk, hs, Tk, F, heads, t0, width, mat);
+  k_align_softmax<<<dim3(rows, heads), 256, 0, st>>>(qk, hs, Tk, F), wh_launched("k_align_softmax");
+  k_align_znorm<<<dim3((F + 63) / 64, heads), 256, 0, st>>>(qk, hs, rows, Tk, F), wh_launched("k_align_znorm");
+  k_align_medmean<<<dim3((F + 255) / 256, N), 256, 0, st>>>(qk, hs, Tk, F, heads, t0, width, mat), wh_launched("k_align_medmean");
 }
 
 void launch_token_probs(const float* logits, int64_t ld, int rows, int eot, const int* tok, float* probs,
                         hipStream_t st) {
-  if (rows > 0) k_token_probs<<<rows, 256, 0, st>>>(logits, ld, eot, tok, probs);
+  if (rows > 0) k_token_probs<<<rows, 256, 0, st>>>(logits, ld, eot, tok, probs), wh_launched("k_token_probs");
 }
 
 }  // namespace wh

@@ -45,6 +45,72 @@ static inline const char* tune_env(const char* name) {
 #endif
 }
 
+// ---------------------------------------------------------------- launch attribution
+// Every kernel launch site is `kernel<<<...>>>(...), wh_launched("kernel");`: the name of
+// the thread's last launch is kept, so a launch error that surfaces later (the entry
+// points check hipGetLastError() once, after their launches) names the launch before it.
+// The tuning build also checks hipGetLastError() after EVERY launch and keeps the first
+// failing launch's name and error (wh_first_launch_error), so the error is attributed to
+// the launch that raised it, not to the entry point that noticed.
+#include <string>
+inline const char*& wh_last_launch() {
+  static thread_local const char* name = "(none)";
+  return name;
+}
+inline std::string& wh_first_launch_error() {
+  static thread_local std::string err;
+  return err;
+}
+inline void wh_launched(const char* name) {
+  wh_last_launch() = name;
+#if WH_TUNING
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess && wh_first_launch_error().empty())
+    wh_first_launch_error() = std::string("launch of ") + name + ": " + hipGetErrorString(e);
+#endif
+}
+
+// Chain trace (tuning build only, profiles/chain_trace.py): per-workgroup wall-clock marks
+// (s_memrealtime, 100 MHz) of the decoder-step kernels, one slot per kernel role; every
+// launch of a role overwrites its slot, so after one step a slot holds that role's LAST
+// launch (layer 31's).  Mark 0 = workgroup start, 1 / 2 = kernel-specific phase ends,
+// 3 = thread 0 done (its stores drained).  Each translation unit has its own copy of the
+// array (static) and reader (WH_CT_READER); the slots of one role live in one unit.
+constexpr int CT_SLOTS = 10, CT_WG = 2048;
+enum { CT_PROJ_QKV = 0, CT_PROJ_NN = 1, CT_PROJ_FC1 = 2, CT_PROJ_FC2 = 3, CT_RESID_LN = 4, CT_REDUCE = 5,
+       CT_SELF_ATTN = 6, CT_XATTN = 7, CT_VOCAB = 8, CT_LOGIT = 9 };
+#if WH_TUNING
+static __device__ unsigned long long g_ct_trace[CT_SLOTS][CT_WG][4];
+#define CT_MARK(slot, k)                                                                 \
+  do {                                                                                   \
+    if (threadIdx.x == 0 && blockIdx.x < CT_WG)                                          \
+      g_ct_trace[slot][blockIdx.x][k] = __builtin_amdgcn_s_memrealtime();                \
+  } while (0)
+#define CT_END(slot)                                       \
+  do {                                                     \
+    if (threadIdx.x == 0) {                                \
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");     \
+      CT_MARK(slot, 3);                                    \
+    }                                                      \
+  } while (0)
+#define WH_CT_READER(name)                                                                        \
+  extern "C" int wh_tune_ct_trace_##name(unsigned long long* out) {                              \
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_ct_trace), sizeof(g_ct_trace)) == hipSuccess ? 0 : -1; \
+  }                                                                                               \
+  extern "C" int wh_tune_ct_clear_##name() {                                                      \
+    static unsigned long long z[CT_SLOTS][CT_WG][4];                                              \
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_ct_trace), z, sizeof(z)) == hipSuccess ? 0 : -1;        \
+  }
+#else
+#define CT_MARK(slot, k) \
+  do {                   \
+  } while (0)
+#define CT_END(slot) \
+  do {               \
+  } while (0)
+#define WH_CT_READER(name)
+#endif
+
 // cross-V (V^T) of a (window, head) is TILE-MAJOR: [TKP / 64 tiles][64 d][64 keys, 32-key permutation],
 // so one 64-key tile's V^T is 8 KB contiguous (one stream, like K's [TKP][64] rows); element (d, t)
 // sits at xv_index(d, t).

@@ -603,6 +603,7 @@ __device__ __forceinline__ void lp_combine(const LPRec* rec, int r, const DecSta
 template <int NS, int LP_EPT, bool FUSED, bool MERGE = false>
 __global__ __launch_bounds__(LP_THREADS) WH_LP_ATTR void k_logit_part(float* __restrict__ logits, int ldl, DecState s,
                                                            DecOpts o, MergeEmbed em) {
+  CT_MARK(CT_LOGIT, 0);
   static_assert(FUSED || !MERGE, "the merge rides on the fused combine");
   constexpr int NWV = LP_THREADS / 64;
   __shared__ __attribute__((aligned(16))) char mlds_raw[MERGE ? sizeof(MergeLds) : 4];
@@ -850,6 +851,7 @@ __global__ __launch_bounds__(LP_THREADS) WH_LP_ATTR void k_logit_part(float* __r
     }
   }  // wave 0
   finish(go);
+  CT_END(CT_LOGIT);
 }
 
 // the merge of a row's NS slice records (in LDS, `rec`) by one wave: the timestamp-rule
@@ -991,32 +993,32 @@ static bool select_rows(float* logits, int ldl, const DecState& s, const DecOpts
   const bool one_win = nwin == 1;
   if (split && fused && !one_win && ns_force == 16 && o.ts_begin > 0 &&
       (o.ts_begin + 14) / 15 <= LP_THREADS * 8 && o.V - o.ts_begin <= LP_THREADS * 8) {
-    if (merge) k_logit_part<16, 8, true, true><<<dim3(rows, 16), LP_THREADS, 0, st>>>(logits, ldl, s, o, e);
-    else k_logit_part<16, 8, true><<<dim3(rows, 16), LP_THREADS, 0, st>>>(logits, ldl, s, o, e);
+    if (merge) k_logit_part<16, 8, true, true><<<dim3(rows, 16), LP_THREADS, 0, st>>>(logits, ldl, s, o, e), wh_launched("k_logit_part");
+    else k_logit_part<16, 8, true><<<dim3(rows, 16), LP_THREADS, 0, st>>>(logits, ldl, s, o, e), wh_launched("k_logit_part");
     return merge;
   }
   if (split && o.ts_begin > 0 && (one_win || ns_force == 32) && (o.ts_begin + 30) / 31 <= LP_THREADS * 4 &&
       o.V - o.ts_begin <= LP_THREADS * 4) {
     if (fused) {
-      if (merge) k_logit_part<32, 4, true, true><<<dim3(rows, 32), LP_THREADS, 0, st>>>(logits, ldl, s, o, e);
-      else k_logit_part<32, 4, true><<<dim3(rows, 32), LP_THREADS, 0, st>>>(logits, ldl, s, o, e);
+      if (merge) k_logit_part<32, 4, true, true><<<dim3(rows, 32), LP_THREADS, 0, st>>>(logits, ldl, s, o, e), wh_launched("k_logit_part");
+      else k_logit_part<32, 4, true><<<dim3(rows, 32), LP_THREADS, 0, st>>>(logits, ldl, s, o, e), wh_launched("k_logit_part");
       return merge;
     }
-    k_logit_part<32, 4, false><<<dim3(rows, 32), LP_THREADS, 0, st>>>(logits, ldl, s, o, e);
-    k_logit_combine<32><<<rows, 64, 0, st>>>(s, o);
+    k_logit_part<32, 4, false><<<dim3(rows, 32), LP_THREADS, 0, st>>>(logits, ldl, s, o, e), wh_launched("k_logit_part");
+    k_logit_combine<32><<<rows, 64, 0, st>>>(s, o), wh_launched("k_logit_combine");
     return false;
   }
   if (split && o.ts_begin > 0 && (o.ts_begin + 6) / 7 <= LP_THREADS * 16 && o.V - o.ts_begin <= LP_THREADS * 16) {
     if (fused) {
-      if (merge) k_logit_part<8, 16, true, true><<<dim3(rows, 8), LP_THREADS, 0, st>>>(logits, ldl, s, o, e);
-      else k_logit_part<8, 16, true><<<dim3(rows, 8), LP_THREADS, 0, st>>>(logits, ldl, s, o, e);
+      if (merge) k_logit_part<8, 16, true, true><<<dim3(rows, 8), LP_THREADS, 0, st>>>(logits, ldl, s, o, e), wh_launched("k_logit_part");
+      else k_logit_part<8, 16, true><<<dim3(rows, 8), LP_THREADS, 0, st>>>(logits, ldl, s, o, e), wh_launched("k_logit_part");
       return merge;
     }
-    k_logit_part<8, 16, false><<<dim3(rows, 8), LP_THREADS, 0, st>>>(logits, ldl, s, o, e);
-    k_logit_combine<8><<<rows, 64, 0, st>>>(s, o);
+    k_logit_part<8, 16, false><<<dim3(rows, 8), LP_THREADS, 0, st>>>(logits, ldl, s, o, e), wh_launched("k_logit_part");
+    k_logit_combine<8><<<rows, 64, 0, st>>>(s, o), wh_launched("k_logit_combine");
     return false;
   }
-  k_logit_rows<<<nwin * s.G, LR_THREADS, 0, st>>>(logits, ldl, s, o);
+  k_logit_rows<<<nwin * s.G, LR_THREADS, 0, st>>>(logits, ldl, s, o), wh_launched("k_logit_rows");
   return false;
 }
 
@@ -1031,7 +1033,7 @@ __global__ __launch_bounds__(256) void k_merge(DecState s, DecOpts o, MergeEmbed
 }
 
 void launch_merge(const DecState& s, const DecOpts& o, int nwin, hipStream_t st, const MergeEmbed& em) {
-  k_merge<<<nwin, 256, 0, st>>>(s, o, em);
+  k_merge<<<nwin, 256, 0, st>>>(s, o, em), wh_launched("k_merge");
 }
 
 void launch_select_merge(float* logits, int ldl, const DecState& s, const DecOpts& o, int nwin, hipStream_t st,
@@ -1542,7 +1544,7 @@ int launch_vocab_select(const GemmArgs& a, const DecState& s, const DecOpts& o, 
   if (!attr) return -5;
   VsArgs v;
   v.s = s; v.o = o; v.em = em; v.rec = rec; v.cnt = cnt;
-  k_vocab_sel<D><<<VS_NB, 512, lds, st>>>(a, v);
+  k_vocab_sel<D><<<VS_NB, 512, lds, st>>>(a, v), wh_launched("k_vocab_sel");
   return 0;
 }
 
@@ -1561,7 +1563,7 @@ __global__ __launch_bounds__(64) void k_append_tokens(DecState s, const int* __r
   if (b == 0) s.len[w] = len + 1;
 }
 void launch_append_tokens(const DecState& s, const int* tok, int nwin, hipStream_t st) {
-  k_append_tokens<<<nwin, 64, 0, st>>>(s, tok);
+  k_append_tokens<<<nwin, 64, 0, st>>>(s, tok), wh_launched("k_append_tokens");
 }
 
 // wh_reorder_kv (rearrange_kv_cache, decoding.py:189-204; rearrange_mkv coreml.mm:251-277):
@@ -1589,7 +1591,7 @@ __global__ __launch_bounds__(256) void k_reorder_rows(DecState s, const int* __r
   }
 }
 void launch_reorder_rows(const DecState& s, const int* src, int nwin, hipStream_t st) {
-  k_reorder_rows<<<nwin, 256, 0, st>>>(s, src);
+  k_reorder_rows<<<nwin, 256, 0, st>>>(s, src), wh_launched("k_reorder_rows");
 }
 
 // ------------------------------------------------------------ no_speech prob (decoding.py:716-720)
@@ -1605,7 +1607,7 @@ __global__ __launch_bounds__(256) void k_no_speech(const float* logits, int ldl,
   if (threadIdx.x == 0) out[blockIdx.x] = __expf(row[ns] - m) / se;
 }
 void launch_no_speech(const float* logits, int ldl, int rows, int V, int ns, float* out, hipStream_t st) {
-  if (rows > 0) k_no_speech<<<rows, 256, 0, st>>>(logits, ldl, V, ns, out);
+  if (rows > 0) k_no_speech<<<rows, 256, 0, st>>>(logits, ldl, V, ns, out), wh_launched("k_no_speech");
 }
 
 __global__ void k_broadcast_rows(const float* src, int ld_src, const int* src_rows, float* dst, int ld_dst, int G,
@@ -1617,7 +1619,11 @@ __global__ void k_broadcast_rows(const float* src, int ld_src, const int* src_ro
 }
 void launch_broadcast_rows(const float* src, int ld_src, const int* src_rows, float* dst, int ld_dst, int G, int nwin,
                            int V, hipStream_t st) {
-  k_broadcast_rows<<<nwin * G, 256, 0, st>>>(src, ld_src, src_rows, dst, ld_dst, G, V);
+  k_broadcast_rows<<<nwin * G, 256, 0, st>>>(src, ld_src, src_rows, dst, ld_dst, G, V), wh_launched("k_broadcast_rows");
 }
 
 }  // namespace wh
+
+#if WH_TUNING
+WH_CT_READER(decode)
+#endif

@@ -794,6 +794,7 @@ __global__ __launch_bounds__(512) void k_vocab1(GemmArgs a) {
 // k_gemv_x: a row's logits are bit-identical whichever kernel the batch size selects.
 template <int MT, int DEPTH>
 __global__ __launch_bounds__(1024) void k_vocab_2p(GemmArgs a) {
+  CT_MARK(CT_VOCAB, 0);
   constexpr int NW = 16, VC = DEPTH > 2 ? 4 : 5, KH = 640, SH = KH / 32, NCH = SH / VC;  // K 1280 (launcher)
   constexpr int XROW = KH * 2 + 16;
   extern __shared__ __attribute__((aligned(16))) char xs2[];
@@ -848,7 +849,10 @@ __global__ __launch_bounds__(1024) void k_vocab_2p(GemmArgs a) {
       }
     }
   }
-  if (!act) return;
+  if (!act) {
+    CT_END(CT_VOCAB);
+    return;
+  }
   // lane holds rows mt*16 + r, columns tile*16 + 4g .. +3
   const int n = tile * 16 + 4 * g;
   const auto rs = wt_rsrc(a.out_f32);
@@ -861,6 +865,7 @@ __global__ __launch_bounds__(1024) void k_vocab_2p(GemmArgs a) {
         if (n + e < a.N) wt_store1(rs, (m * a.ldo + n + e) * 4, acc[mt][e] + (a.bias ? a.bias[n + e] : 0.f));
     }
   }
+  CT_END(CT_VOCAB);
 }
 
 // ============================================================ tall-skinny GEMM, X through LDS
@@ -1034,8 +1039,8 @@ int launch_gemm_tiles(const GemmArgs& a, int epi, int tile_sel, hipStream_t st) 
     switch (epi) {
 #define CASE(E)                                                   \
   case E:                                                         \
-    if (tile_sel == 257) k_gemm_256<E, 32><<<nwg, 512, 0, st>>>(a); \
-    else k_gemm_256<E><<<nwg, 512, 0, st>>>(a);                    \
+    if (tile_sel == 257) k_gemm_256<E, 32><<<nwg, 512, 0, st>>>(a), wh_launched("k_gemm_256"); \
+    else k_gemm_256<E><<<nwg, 512, 0, st>>>(a), wh_launched("k_gemm_256");                    \
     break;
       CASE(EPI_STORE) CASE(EPI_STORE_GELU) CASE(EPI_RESID) CASE(EPI_GELU_POS) CASE(EPI_HEADSPLIT) CASE(EPI_QKV_ENC)
 #undef CASE
@@ -1052,15 +1057,15 @@ int launch_gemm_tiles(const GemmArgs& a, int epi, int tile_sel, hipStream_t st) 
     const bool kz2 = half && sizeof(T) == 2 && (epi == EPI_RESID || epi == EPI_GELU_POS) && a.p1_slab && a.p1_cnt &&
                      (a.K / (TKB / (int)sizeof(T))) % 2 == 0 && (int64_t)nwg * 64 <= a.p1_slabs && tile_sel != 128;
     if (kz2) {
-      if (epi == EPI_RESID) k_gemm_tile<T, EPI_RESID, 64, 2><<<2 * nwg, 256, 0, st>>>(a);
-      else k_gemm_tile<T, EPI_GELU_POS, 64, 2><<<2 * nwg, 256, 0, st>>>(a);
+      if (epi == EPI_RESID) k_gemm_tile<T, EPI_RESID, 64, 2><<<2 * nwg, 256, 0, st>>>(a), wh_launched("k_gemm_tile");
+      else k_gemm_tile<T, EPI_GELU_POS, 64, 2><<<2 * nwg, 256, 0, st>>>(a), wh_launched("k_gemm_tile");
       return 0;
     }
     switch (epi) {
 #define CASE(E)                                                       \
   case E:                                                             \
-    if (half) k_gemm_tile<T, E, 64><<<nwg, 256, 0, st>>>(a);          \
-    else k_gemm_tile<T, E><<<nwg, 256, 0, st>>>(a);                   \
+    if (half) k_gemm_tile<T, E, 64><<<nwg, 256, 0, st>>>(a), wh_launched("k_gemm_tile");          \
+    else k_gemm_tile<T, E><<<nwg, 256, 0, st>>>(a), wh_launched("k_gemm_tile");                   \
     break;
       CASE(EPI_STORE) CASE(EPI_STORE_GELU) CASE(EPI_RESID) CASE(EPI_GELU_POS) CASE(EPI_HEADSPLIT) CASE(EPI_QKV_DEC)
       CASE(EPI_QKV_ENC)
@@ -1093,7 +1098,7 @@ int launch_gemm_tiles(const GemmArgs& a, int epi, int tile_sel, hipStream_t st) 
       static bool attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_vocab1<D>),
                                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) == hipSuccess;
       if (!attr) return -5;
-      k_vocab1<D><<<256, 512, lds, st>>>(a);
+      k_vocab1<D><<<256, 512, lds, st>>>(a), wh_launched("k_vocab1");
       return 0;
     }
     // k_vocab_small: the rows in groups of <= 64 that fit LDS with all of K (152 KB)
@@ -1114,7 +1119,7 @@ int launch_gemm_tiles(const GemmArgs& a, int epi, int tile_sel, hipStream_t st) 
         static bool attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_vocab_small<T, MTV>),
                                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) == hipSuccess;
         if (!attr) return -5;
-        k_vocab_small<T, MTV><<<grid, 512, lds, st>>>(av);
+        k_vocab_small<T, MTV><<<grid, 512, lds, st>>>(av), wh_launched("k_vocab_small");
         return 0;
       };
       switch (mtv) {
@@ -1142,8 +1147,8 @@ int launch_gemm_tiles(const GemmArgs& a, int epi, int tile_sel, hipStream_t st) 
                            hipFuncSetAttribute(reinterpret_cast<const void*>(&k_vocab_2p<MTV, 3>),
                                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) == hipSuccess;
         if (!attr) return -5;
-        if (d3) k_vocab_2p<MTV, 3><<<grid, 1024, lds, st>>>(a);
-        else k_vocab_2p<MTV, 2><<<grid, 1024, lds, st>>>(a);
+        if (d3) k_vocab_2p<MTV, 3><<<grid, 1024, lds, st>>>(a), wh_launched("k_vocab_2p");
+        else k_vocab_2p<MTV, 2><<<grid, 1024, lds, st>>>(a), wh_launched("k_vocab_2p");
         return 0;
       };
       switch ((a.M + 15) / 16) {
@@ -1165,8 +1170,8 @@ int launch_gemm_tiles(const GemmArgs& a, int epi, int tile_sel, hipStream_t st) 
       dim3 gv((a.N + 16 * nw - 1) / (16 * nw), (a.M + 16 * rows_per - 1) / (16 * rows_per), 1);
 #define LAUNCHV(MT_)                                                                                  \
   switch (nw) {                                                                                      \
-    case 4: k_gemv_x<T, MT_, EPI_F32_COLS, 4><<<gv, 256, 0, st>>>(a); break;                         \
-    default: k_gemv_x<T, MT_, EPI_F32_COLS, 8><<<gv, 512, 0, st>>>(a); break;                        \
+    case 4: k_gemv_x<T, MT_, EPI_F32_COLS, 4><<<gv, 256, 0, st>>>(a), wh_launched("k_gemv_x"); break;                         \
+    default: k_gemv_x<T, MT_, EPI_F32_COLS, 8><<<gv, 512, 0, st>>>(a), wh_launched("k_gemv_x"); break;                        \
   }
       switch (rows_per) {
         case 3: LAUNCHV(3) break;
@@ -1188,12 +1193,12 @@ int launch_gemm_tiles(const GemmArgs& a, int epi, int tile_sel, hipStream_t st) 
       dim3 gx((a.N + 63) / 64, (a.M + 16 * rows_per - 1) / (16 * rows_per), ks);
 #define LAUNCHX(MT_)                                                                            \
   switch (epi) {                                                                               \
-    case EPI_STORE: k_gemv_x<T, MT_, EPI_STORE><<<gx, 256, 0, st>>>(a); break;                  \
-    case EPI_STORE_GELU: k_gemv_x<T, MT_, EPI_STORE_GELU><<<gx, 256, 0, st>>>(a); break;        \
-    case EPI_RESID: k_gemv_x<T, MT_, EPI_RESID><<<gx, 256, 0, st>>>(a); break;                  \
-    case EPI_QKV_DEC: k_gemv_x<T, MT_, EPI_QKV_DEC><<<gx, 256, 0, st>>>(a); break;              \
-    case EPI_F32_COLS: k_gemv_x<T, MT_, EPI_F32_COLS><<<gx, 256, 0, st>>>(a); break;            \
-    case EPI_PARTIAL: k_gemv_x<T, MT_, EPI_PARTIAL><<<gx, 256, 0, st>>>(a); break;              \
+    case EPI_STORE: k_gemv_x<T, MT_, EPI_STORE><<<gx, 256, 0, st>>>(a), wh_launched("k_gemv_x"); break;                  \
+    case EPI_STORE_GELU: k_gemv_x<T, MT_, EPI_STORE_GELU><<<gx, 256, 0, st>>>(a), wh_launched("k_gemv_x"); break;        \
+    case EPI_RESID: k_gemv_x<T, MT_, EPI_RESID><<<gx, 256, 0, st>>>(a), wh_launched("k_gemv_x"); break;                  \
+    case EPI_QKV_DEC: k_gemv_x<T, MT_, EPI_QKV_DEC><<<gx, 256, 0, st>>>(a), wh_launched("k_gemv_x"); break;              \
+    case EPI_F32_COLS: k_gemv_x<T, MT_, EPI_F32_COLS><<<gx, 256, 0, st>>>(a), wh_launched("k_gemv_x"); break;            \
+    case EPI_PARTIAL: k_gemv_x<T, MT_, EPI_PARTIAL><<<gx, 256, 0, st>>>(a), wh_launched("k_gemv_x"); break;              \
     default: return -1;                                                                        \
   }
       switch (rows_per) {
@@ -1210,13 +1215,13 @@ int launch_gemm_tiles(const GemmArgs& a, int epi, int tile_sel, hipStream_t st) 
     dim3 grid((a.N + 15) / 16, (a.M + 16 * rows_per - 1) / (16 * rows_per), ks);
 #define LAUNCH(MT_)                                                                             \
   switch (epi) {                                                                               \
-    case EPI_STORE: k_gemv_rows<T, MT_, EPI_STORE><<<grid, 512, 0, st>>>(a); break;             \
-    case EPI_STORE_GELU: k_gemv_rows<T, MT_, EPI_STORE_GELU><<<grid, 512, 0, st>>>(a); break;   \
-    case EPI_RESID: k_gemv_rows<T, MT_, EPI_RESID><<<grid, 512, 0, st>>>(a); break;             \
-    case EPI_HEADSPLIT: k_gemv_rows<T, MT_, EPI_HEADSPLIT><<<grid, 512, 0, st>>>(a); break;     \
-    case EPI_QKV_DEC: k_gemv_rows<T, MT_, EPI_QKV_DEC><<<grid, 512, 0, st>>>(a); break;         \
-    case EPI_F32_COLS: k_gemv_rows<T, MT_, EPI_F32_COLS><<<grid, 512, 0, st>>>(a); break;       \
-    case EPI_PARTIAL: k_gemv_rows<T, MT_, EPI_PARTIAL><<<grid, 512, 0, st>>>(a); break;         \
+    case EPI_STORE: k_gemv_rows<T, MT_, EPI_STORE><<<grid, 512, 0, st>>>(a), wh_launched("k_gemv_rows"); break;             \
+    case EPI_STORE_GELU: k_gemv_rows<T, MT_, EPI_STORE_GELU><<<grid, 512, 0, st>>>(a), wh_launched("k_gemv_rows"); break;   \
+    case EPI_RESID: k_gemv_rows<T, MT_, EPI_RESID><<<grid, 512, 0, st>>>(a), wh_launched("k_gemv_rows"); break;             \
+    case EPI_HEADSPLIT: k_gemv_rows<T, MT_, EPI_HEADSPLIT><<<grid, 512, 0, st>>>(a), wh_launched("k_gemv_rows"); break;     \
+    case EPI_QKV_DEC: k_gemv_rows<T, MT_, EPI_QKV_DEC><<<grid, 512, 0, st>>>(a), wh_launched("k_gemv_rows"); break;         \
+    case EPI_F32_COLS: k_gemv_rows<T, MT_, EPI_F32_COLS><<<grid, 512, 0, st>>>(a), wh_launched("k_gemv_rows"); break;       \
+    case EPI_PARTIAL: k_gemv_rows<T, MT_, EPI_PARTIAL><<<grid, 512, 0, st>>>(a), wh_launched("k_gemv_rows"); break;         \
     default: return -1;                                                                        \
   }
     switch (rows_per) {
@@ -1239,3 +1244,7 @@ template int launch_gemm_tiles<half_t>(const GemmArgs&, int, int, hipStream_t);
 template int launch_gemm<half_t>(const GemmArgs&, int, hipStream_t);
 
 }  // namespace wh
+
+#if WH_TUNING
+WH_CT_READER(gemm)
+#endif

@@ -126,6 +126,8 @@ void launch_merge(const DecState& s, const DecOpts& o, int nwin, hipStream_t st,
 // LayerNorm, selection, merge) in one launch; -1 when the shape does not fit it
 struct GemmArgs;
 bool vocab_select_on();
+int self_attn_grp_mode();
+bool self_attn_pipe_on();
 int launch_vocab_select(const GemmArgs& a, const DecState& s, const DecOpts& o, const MergeEmbed& em, float* rec,
                         int* cnt, hipStream_t st);
 constexpr size_t VS_REC_FLOATS = 8 * 2 * 256 * 32;  // k_vocab_sel records [rows][part][workgroup][32]

@@ -61,7 +61,7 @@ template <typename T>
 void launch_layernorm(const float* x, T* y, const float* g, const float* b, int rows, int n, float eps,
                       const int* rows_in, hipStream_t st) {
   if (rows <= 0) return;
-  k_layernorm<T><<<(rows + 3) / 4, 256, 0, st>>>(x, y, g, b, rows, n, eps, rows_in);
+  k_layernorm<T><<<(rows + 3) / 4, 256, 0, st>>>(x, y, g, b, rows, n, eps, rows_in), wh_launched("k_layernorm");
 }
 
 // x[r] += bias + sum_s part[s][r] (fixed order: deterministic split-K reduction of the
@@ -74,6 +74,7 @@ __global__ __launch_bounds__(512) void k_resid_ln(float* __restrict__ x, const S
                                                   const float* __restrict__ beta, int n, float eps) {
   __shared__ float red[2][8];
   const int row = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, NT = blockDim.x, nwv = NT >> 6;
+  CT_MARK(CT_RESID_LN, 0);
   float* xr = x + (int64_t)row * n;
   // NT * 4 * MAXV >= n (n <= 2048): 256 threads x 2 float4, or ceil(n / 256) waves x 1
   const int nv = n >> 2;
@@ -110,6 +111,7 @@ __global__ __launch_bounds__(512) void k_resid_ln(float* __restrict__ x, const S
   s = wave_sum(s);
   if (lane == 0) red[0][wv] = s;
   __syncthreads();
+  CT_MARK(CT_RESID_LN, 1);
   float tot = 0.f;
   for (int k = 0; k < nwv; ++k) tot += red[0][k];
   const float mean = tot / (float)n;
@@ -137,6 +139,7 @@ __global__ __launch_bounds__(512) void k_resid_ln(float* __restrict__ x, const S
       store4(yr + 4 * c, (v[i][0] - mean) * rstd * gm[i][0] + bt[i][0], (v[i][1] - mean) * rstd * gm[i][1] + bt[i][1],
              (v[i][2] - mean) * rstd * gm[i][2] + bt[i][2], (v[i][3] - mean) * rstd * gm[i][3] + bt[i][3]);
   }
+  CT_END(CT_RESID_LN);
 }
 
 template <typename T>
@@ -149,12 +152,12 @@ void launch_resid_ln(float* x, const float* part, int nsplit, int64_t part_strid
   const int nt = (e && atoi(e) == 1) ? 256 : ((n >> 2) + 63) / 64 * 64;
   if (slab_half && nsplit > 0 && nt != 256) {  // fp16 slabs (fp16 contexts, k_proj)
     const half_t* ph = reinterpret_cast<const half_t*>(part);
-    if (nsplit <= 4) k_resid_ln<T, 4, 1, half_t><<<rows, nt, 0, st>>>(x, ph, nsplit, part_stride, bias, y, g, b, n, eps);
-    else k_resid_ln<T, 16, 1, half_t><<<rows, nt, 0, st>>>(x, ph, nsplit, part_stride, bias, y, g, b, n, eps);
+    if (nsplit <= 4) k_resid_ln<T, 4, 1, half_t><<<rows, nt, 0, st>>>(x, ph, nsplit, part_stride, bias, y, g, b, n, eps), wh_launched("k_resid_ln");
+    else k_resid_ln<T, 16, 1, half_t><<<rows, nt, 0, st>>>(x, ph, nsplit, part_stride, bias, y, g, b, n, eps), wh_launched("k_resid_ln");
     return;
   }
 #define RLN(NS_, MV_) \
-  k_resid_ln<T, NS_, MV_><<<rows, nt, 0, st>>>(x, part, NS_ ? nsplit : 0, part_stride, bias, y, g, b, n, eps)
+  k_resid_ln<T, NS_, MV_><<<rows, nt, 0, st>>>(x, part, NS_ ? nsplit : 0, part_stride, bias, y, g, b, n, eps), wh_launched("k_resid_ln")
   if (nsplit <= 0) {
     if (nt == 256) RLN(0, 2); else RLN(0, 1);
   } else if (nsplit <= 4) {
@@ -348,10 +351,10 @@ void launch_attn_enc(const T* qkv, int ld, int ns, int H, int Tlen, int nwin, in
   const int blocks8 = (Tlen + 127) / 128 * H * nwin;
   if (blocks8 < 512) {
     dim3 grid((Tlen + 63) / 64, H, nwin);
-    k_attn_enc<T, 4><<<grid, 256, 0, st>>>(qkv, ld, ns, Tlen, wsi, vt, tkp, out, wso);
+    k_attn_enc<T, 4><<<grid, 256, 0, st>>>(qkv, ld, ns, Tlen, wsi, vt, tkp, out, wso), wh_launched("k_attn_enc");
   } else {
     dim3 grid((Tlen + 127) / 128, H, nwin);
-    k_attn_enc<T, 8><<<grid, 512, 0, st>>>(qkv, ld, ns, Tlen, wsi, vt, tkp, out, wso);
+    k_attn_enc<T, 8><<<grid, 512, 0, st>>>(qkv, ld, ns, Tlen, wsi, vt, tkp, out, wso), wh_launched("k_attn_enc");
   }
 }
 
@@ -609,11 +612,11 @@ void launch_self_attn(const T* q, int ldq, const T* kc, const T* vc, const int* 
   if constexpr (sizeof(T) == 2) {
     if (pipe) {
       k_self_attn<T, true><<<dim3(rows, H), 64, 0, st>>>(q, ldq, kc, vc, rw, rs, rp, anc, anc_beams, nbeam, H, ctx, out,
-                                                         ldo);
+                                                         ldo), wh_launched("k_self_attn");
       return;
     }
   }
-  k_self_attn<T><<<dim3(rows, H), 64, 0, st>>>(q, ldq, kc, vc, rw, rs, rp, anc, anc_beams, nbeam, H, ctx, out, ldo);
+  k_self_attn<T><<<dim3(rows, H), 64, 0, st>>>(q, ldq, kc, vc, rw, rs, rp, anc, anc_beams, nbeam, H, ctx, out, ldo), wh_launched("k_self_attn");
 }
 
 // Step-mode variant: the QKV projection arrives as split-K fp32 partial slabs
@@ -642,6 +645,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void
   __shared__ int slot_of[512];
   __shared__ float qs[64], vs[64];
   const int lane = threadIdx.x, G = anc_beams;
+  CT_MARK(CT_SELF_ATTN, 0);
   // step rows: window w = row / G, beam slot = row % G (row_win / row_slot hold the same)
   const int L = xcd_remap(blockIdx.x, gridDim.x), sl = L % G, wh = L / G, h = wh % H, w = wh / H, row = w * G + sl;
   const int* an = anc + ((int64_t)w * anc_beams + sl) * ctx;
@@ -756,6 +760,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void
       store4(op, o[0], o[1], o[2], o[3]);
       store4(op + 4, o[4], o[5], o[6], o[7]);
     }
+    CT_END(CT_SELF_ATTN);
     return;
   }
   float qv[64];
@@ -824,6 +829,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void
       store4(op, o[0], o[1], o[2], o[3]);
       store4(op + 4, o[4], o[5], o[6], o[7]);
     }
+    CT_END(CT_SELF_ATTN);
     return;
   }
   // fp32 (parity context): scores of the cached positions p < pos: lane per key, two
@@ -902,6 +908,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void
     store4(op, o[0], o[1], o[2], o[3]);
     store4(op + 4, o[4], o[5], o[6], o[7]);
   }
+  CT_END(CT_SELF_ATTN);
 }
 
 // Grouped form (fp16, a window's G <= 8 beams as the G waves of one workgroup per
@@ -1097,6 +1104,25 @@ __global__ __launch_bounds__(64 * SA_GMAX) void k_self_attn_grp(const float* __r
   }
 }
 
+// the self-attention form launch_self_attn_qkv picks (also what wh_step_kernels reports):
+// the grouped form only in the tuning build with WHISPER_HIP_SA_GRP set; the pipelined
+// 64-key passes unless WHISPER_HIP_SA_PIPE=0 (tuning build)
+int self_attn_grp_mode() {
+  static const int grp = [] {
+    const char* e = tune_env("WHISPER_HIP_SA_GRP");
+    return e ? atoi(e) : 0;
+  }();
+  return grp;
+}
+bool self_attn_pipe_on() {
+  static const bool pipe = [] {
+    const char* e = tune_env("WHISPER_HIP_SA_PIPE");
+    return !(e && e[0] == '0');
+  }();
+  return pipe;
+}
+
+
 template <typename T>
 int launch_self_attn_qkv(const float* part, int nsplit, int64_t part_stride, const float* bqkv, int ns, T* kc, T* vc,
                           const int* rw, const int* rs, const int* rp, const int* anc, int anc_beams, int nbeam, int H,
@@ -1113,37 +1139,31 @@ int launch_self_attn_qkv(const float* part, int nsplit, int64_t part_stride, con
   // WHISPER_HIP_SA_GRP=2: 64-key passes, 132 VGPRs, one round — slower still (3.423 -> 3.523
   // ms at 12 tokens, 3.819 -> 4.145 at 220, profiles/r04/self_attn_grp64_ab.txt): the
   // growth with the context is the passes' round trips, not the bytes the beams share
-  static const int grp = [] {
-    const char* e = tune_env("WHISPER_HIP_SA_GRP");
-    return e ? atoi(e) : 0;
-  }();
+  const int grp = self_attn_grp_mode();
   if constexpr (sizeof(T) == 2) {
     if (grp && anc_beams >= 2 && anc_beams <= SA_GMAX && ctx <= 512) {
       if (grp == 2)
         k_self_attn_grp<T, 64><<<(rows / anc_beams) * H, 64 * anc_beams, 0, st>>>(
-            part, nsplit, part_stride, bqkv, ns, kc, vc, rp, anc, anc_beams, nbeam, H, ctx, out, ldo);
+            part, nsplit, part_stride, bqkv, ns, kc, vc, rp, anc, anc_beams, nbeam, H, ctx, out, ldo), wh_launched("k_self_attn_grp");
       else
         k_self_attn_grp<T, 128><<<(rows / anc_beams) * H, 64 * anc_beams, 0, st>>>(
-            part, nsplit, part_stride, bqkv, ns, kc, vc, rp, anc, anc_beams, nbeam, H, ctx, out, ldo);
+            part, nsplit, part_stride, bqkv, ns, kc, vc, rp, anc, anc_beams, nbeam, H, ctx, out, ldo), wh_launched("k_self_attn_grp");
       return 0;
     }
   }
   // fp16: the pipelined 64-key passes (WHISPER_HIP_SA_PIPE=0 in the tuning build: the
   // 128-key passes): 20-window step 3.419 -> 3.363 ms at 12 tokens, 3.810 -> 3.756 at 220,
   // config 3 675.6 -> 684.6 xRT (profiles/r04/self_attn_pipe_ab.txt)
-  static const bool pipe = [] {
-    const char* e = tune_env("WHISPER_HIP_SA_PIPE");
-    return !(e && e[0] == '0');
-  }();
+  const bool pipe = self_attn_pipe_on();
   if constexpr (sizeof(T) == 2) {
     if (pipe) {
       k_self_attn_qkv<T, true><<<rows * H, 64, 0, st>>>(part, nsplit, part_stride, bqkv, ns, kc, vc, rw, rs, rp, anc,
-                                                       anc_beams, nbeam, H, ctx, out, ldo);
+                                                       anc_beams, nbeam, H, ctx, out, ldo), wh_launched("k_self_attn_qkv");
       return 0;
     }
   }
   k_self_attn_qkv<T><<<rows * H, 64, 0, st>>>(part, nsplit, part_stride, bqkv, ns, kc, vc, rw, rs, rp, anc, anc_beams,
-                                             nbeam, H, ctx, out, ldo);
+                                             nbeam, H, ctx, out, ldo), wh_launched("k_self_attn_qkv");
   return 0;
 }
 
@@ -1154,6 +1174,7 @@ __global__ __launch_bounds__(256) void k_reduce_store(const S* __restrict__ part
                                                       const float* __restrict__ bias, T* __restrict__ out, int ldo, int M,
                                                       int N) {
   const int64_t i = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4;
+  CT_MARK(CT_REDUCE, 0);
   if (i >= (int64_t)M * N) return;
   const int m = (int)(i / N), n = (int)(i - (int64_t)m * N);
   typedef typename std::conditional<sizeof(S) == 2, half4_t, float4_t>::type R4;  // raw slab elements
@@ -1170,6 +1191,7 @@ __global__ __launch_bounds__(256) void k_reduce_store(const S* __restrict__ part
     for (int j = 0; j < 4; ++j) v[j] = gelu_f(v[j]);
   }
   store4(out + (int64_t)m * ldo + n, v[0], v[1], v[2], v[3]);
+  CT_END(CT_REDUCE);
 }
 
 template <typename T>
@@ -1180,12 +1202,12 @@ void launch_reduce_store(const float* part, int nsplit, int64_t part_stride, con
   const unsigned nb = (unsigned)((tot + 255) / 256);
   if (slab_half) {
     const half_t* ph = reinterpret_cast<const half_t*>(part);
-    if (gelu) k_reduce_store<T, 1, half_t><<<nb, 256, 0, st>>>(ph, nsplit, part_stride, bias, out, ldo, M, N);
-    else k_reduce_store<T, 0, half_t><<<nb, 256, 0, st>>>(ph, nsplit, part_stride, bias, out, ldo, M, N);
+    if (gelu) k_reduce_store<T, 1, half_t><<<nb, 256, 0, st>>>(ph, nsplit, part_stride, bias, out, ldo, M, N), wh_launched("k_reduce_store");
+    else k_reduce_store<T, 0, half_t><<<nb, 256, 0, st>>>(ph, nsplit, part_stride, bias, out, ldo, M, N), wh_launched("k_reduce_store");
     return;
   }
-  if (gelu) k_reduce_store<T, 1><<<nb, 256, 0, st>>>(part, nsplit, part_stride, bias, out, ldo, M, N);
-  else k_reduce_store<T, 0><<<nb, 256, 0, st>>>(part, nsplit, part_stride, bias, out, ldo, M, N);
+  if (gelu) k_reduce_store<T, 1><<<nb, 256, 0, st>>>(part, nsplit, part_stride, bias, out, ldo, M, N), wh_launched("k_reduce_store");
+  else k_reduce_store<T, 0><<<nb, 256, 0, st>>>(part, nsplit, part_stride, bias, out, ldo, M, N), wh_launched("k_reduce_store");
 }
 
 // ============================================================ decoder cross-attention (split-K flash decoding)
@@ -1466,6 +1488,7 @@ __global__ __launch_bounds__(512, 1) void k_xattn_seg(const T* __restrict__ q, i
   const int s0 = (int)((int64_t)b * nseg / nwg), s1 = (int)((int64_t)(b + 1) * nseg / nwg), cnt = s1 - s0;
   const int pa = s0 / nsp, plast = (s1 - 1) / nsp;
   XS_MARK(0);
+  CT_MARK(CT_XATTN, 0);
 
   // local tile i: K and V fragments
   auto load_kv = [&](int i, Frag<T>(&kf)[4][2], Frag<T>(&vf)[4][2]) {
@@ -1670,6 +1693,7 @@ __global__ __launch_bounds__(512, 1) void k_xattn_seg(const T* __restrict__ q, i
   }
   __syncthreads();
   XS_MARK(5);
+  CT_MARK(CT_XATTN, 3);
   if (part > 1 || !s_ticket[part]) return;
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // no instruction: keeps the loads below the add
   const int pj = part ? plast : pa;
@@ -1686,6 +1710,7 @@ __global__ __launch_bounds__(512, 1) void k_xattn_seg(const T* __restrict__ q, i
 
 #if WH_TUNING
 }  // namespace wh
+WH_CT_READER(kernels)
 extern "C" int wh_tune_xs_trace(unsigned long long* out) {
   return hipMemcpyFromSymbol(out, HIP_SYMBOL(wh::g_xs_trace), sizeof(wh::g_xs_trace)) == hipSuccess ? 0 : -1;
 }
@@ -1740,10 +1765,10 @@ void launch_cross_attn(const T* q, int ldq, const T* ck, const T* cv, int Tk, in
 #define XSF(QZ_, RR_, S_)                                                                                         \
   if (full)                                                                                                     \
     k_xattn_seg<T, QZ_, RR_, S_, true><<<nwg_xs, 512, 0, st>>>(q, ldq, ck, cv, Tk, H, npair, nsp, win_row0,       \
-                                                               win_nrows, win_slot, win_stride, xq, out, ldo);   \
+                                                               win_nrows, win_slot, win_stride, xq, out, ldo), wh_launched("k_xattn_seg");   \
   else                                                                                                          \
     k_xattn_seg<T, QZ_, RR_, S_, false><<<nwg_xs, 512, 0, st>>>(q, ldq, ck, cv, Tk, H, npair, nsp, win_row0,      \
-                                                                win_nrows, win_slot, win_stride, xq, out, ldo)
+                                                                win_nrows, win_slot, win_stride, xq, out, ldo), wh_launched("k_xattn_seg")
 #define XS(QZ_, RR_)          \
   if (xq.part_half) {         \
     XSF(QZ_, RR_, half_t);    \
@@ -1779,7 +1804,7 @@ void launch_cross_attn(const T* q, int ldq, const T* ck, const T* cv, int Tk, in
   const dim3 grid(nwin, H, nsplit);
 #define XA(QZ_)                                                                                          \
   k_cross_attn<T, NW, QZ_><<<grid, 64 * NW, 0, st>>>(q, ldq, ck, cv, Tk, H, nsplit, win_row0, win_nrows, win_slot, \
-                                                     win_stride, po, pm, pl, qk_out, qk_map, qk_rows, xq)
+                                                     win_stride, po, pm, pl, qk_out, qk_map, qk_rows, xq), wh_launched("k_cross_attn")
   switch (xq.part ? xq.z : 0) {
     case 4: XA(4); break;
     case 8: XA(8); break;
@@ -1787,7 +1812,7 @@ void launch_cross_attn(const T* q, int ldq, const T* ck, const T* cv, int Tk, in
     default: XA(0); break;
   }
 #undef XA
-  k_cross_combine<T><<<dim3(rows, H), 64, 0, st>>>(po, pm, pl, H, nsplit, out, ldo);
+  k_cross_combine<T><<<dim3(rows, H), 64, 0, st>>>(po, pm, pl, H, nsplit, out, ldo), wh_launched("k_cross_combine");
 }
 
 // ============================================================ embedding
@@ -1817,7 +1842,7 @@ template <typename T>
 void launch_embed(const T* E, const T* P, int n, const int* row_tok, int* row_pos, const int* hist,
                   const int* cur_len, int G, int hctx, int pmax, float* x, int rows, hipStream_t st) {
   if (rows <= 0) return;
-  k_embed<T><<<rows, 256, 0, st>>>(E, P, n, row_tok, row_pos, hist, cur_len, G, hctx, pmax, x);
+  k_embed<T><<<rows, 256, 0, st>>>(E, P, n, row_tok, row_pos, hist, cur_len, G, hctx, pmax, x), wh_launched("k_embed");
 }
 
 // ============================================================ encoder input prep
@@ -1842,7 +1867,7 @@ __global__ void k_mel_windows(const float* __restrict__ mel, int64_t ld_mel, int
 template <typename T>
 void launch_mel_windows(const float* mel, int64_t ld_mel, int n_mels, const int64_t* seeks, const int* segs, T* melT,
                         int64_t win_stride, int rows_alloc, int nwin, hipStream_t st) {
-  k_mel_windows<T><<<dim3(64, nwin), 256, 0, st>>>(mel, ld_mel, n_mels, seeks, segs, melT, win_stride, rows_alloc);
+  k_mel_windows<T><<<dim3(64, nwin), 256, 0, st>>>(mel, ld_mel, n_mels, seeks, segs, melT, win_stride, rows_alloc), wh_launched("k_mel_windows");
 }
 
 // zero pad rows around the conv1 output (rows 0 and 3001 of each window)
@@ -1856,7 +1881,7 @@ __global__ void k_zero_rows(T* buf, int64_t win_stride, int n, int row_a, int ro
 }
 template <typename T>
 void launch_zero_rows(T* buf, int64_t ws, int n, int ra, int rb, int nwin, hipStream_t st) {
-  k_zero_rows<T><<<nwin, 256, 0, st>>>(buf, ws, n, ra, rb);
+  k_zero_rows<T><<<nwin, 256, 0, st>>>(buf, ws, n, ra, rb), wh_launched("k_zero_rows");
 }
 
 // ============================================================ log-mel spectrogram
@@ -1946,11 +1971,11 @@ void launch_mel(const float* audio, int64_t n_real, int64_t n_padded, int64_t fr
                 const float* filters, int n_mels, float* mel, int64_t ld, unsigned* gmax, hipStream_t st) {
   const int64_t nb = (count + MEL_FB - 1) / MEL_FB;
   if (nb > 0)
-    k_mel_frames<<<(unsigned)nb, 256, 0, st>>>(audio, n_real, n_padded, frame0 + count, frame0, filters, n_mels, mel, ld, gmax);
+    k_mel_frames<<<(unsigned)nb, 256, 0, st>>>(audio, n_real, n_padded, frame0 + count, frame0, filters, n_mels, mel, ld, gmax), wh_launched("k_mel_frames");
 }
 void launch_mel_norm(float* mel, int64_t count, int64_t ld, int n_mels, const unsigned* gmax, const float* ovr,
                      hipStream_t st) {
-  k_mel_norm<<<1024, 256, 0, st>>>(mel, count, ld, n_mels, gmax, ovr);
+  k_mel_norm<<<1024, 256, 0, st>>>(mel, count, ld, n_mels, gmax, ovr), wh_launched("k_mel_norm");
 }
 
 // explicit instantiations

@@ -55,6 +55,8 @@ __global__ __launch_bounds__(64 * NSUB * KW) void k_proj(GemmArgs a) {
 #endif
   const int kb = kz * P::KC;
   const int n0 = ct * P::CT + sub * 16, m0 = mg * P::MR;
+  const int ct_slot = a.N == a.K ? CT_PROJ_NN : a.N == 3 * a.K ? CT_PROJ_QKV : a.N == 4 * a.K ? CT_PROJ_FC1 : CT_PROJ_FC2;
+  CT_MARK(ct_slot, 0);
 
   // 1. X slice -> registers
   const char* X = reinterpret_cast<const char*>(a.X);
@@ -94,6 +96,7 @@ __global__ __launch_bounds__(64 * NSUB * KW) void k_proj(GemmArgs a) {
     }
   }
   __syncthreads();
+  CT_MARK(ct_slot, 1);
 
   float4_t acc[MT];
 #pragma unroll
@@ -108,6 +111,7 @@ __global__ __launch_bounds__(64 * NSUB * KW) void k_proj(GemmArgs a) {
       mfma_step(acc[mt], wf[s], xf);
     }
   }
+  CT_MARK(ct_slot, 2);
 
   // fixed-order reduction of the KW wave tiles
   if constexpr (KW > 1) {
@@ -160,6 +164,7 @@ __global__ __launch_bounds__(64 * NSUB * KW) void k_proj(GemmArgs a) {
       epilogue_store<T, EPI>(a, m, 0, m, n, v);
     }
   }
+  CT_END(ct_slot);
 }
 
 // ------------------------------------------------------------ single-window step layer

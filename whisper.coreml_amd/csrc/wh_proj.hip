@@ -118,9 +118,11 @@ int launch_proj_partial(const GemmArgs& a, int max_z, hipStream_t st, int* z_out
   GemmArgs b = a;
   b.ksplit = best_z;
   if (ev0)
-    hipExtLaunchKernelGGL(e.f, dim3(best_wgs), dim3(64 * CFGS[best].nsub * CFGS[best].kw), e.lds, st, ev0, ev1, 0, b);
-  else
+    hipExtLaunchKernelGGL(e.f, dim3(best_wgs), dim3(64 * CFGS[best].nsub * CFGS[best].kw), e.lds, st, ev0, ev1, 0, b), wh_launched("k_proj");
+  else {
     hipLaunchKernelGGL(e.f, dim3(best_wgs), dim3(64 * CFGS[best].nsub * CFGS[best].kw), e.lds, st, b);
+    wh_launched("k_proj");
+  }
   *z_out = best_z;
   return 0;
 }
@@ -148,9 +150,11 @@ int p1_go(const GemmArgs& a, hipStream_t st, hipEvent_t ev0, hipEvent_t ev1) {
   const dim3 grid(a.N / (16 * NSUB), ZS), block(64 * NSUB * KW);
   void (*f)(GemmArgs) = &k_proj1<T, NSUB, KW, NS, ZS, CPL, EPI, MODE>;
   if (ev0)
-    hipExtLaunchKernelGGL(f, grid, block, P::LDS, st, ev0, ev1, 0, a);
-  else
+    hipExtLaunchKernelGGL(f, grid, block, P::LDS, st, ev0, ev1, 0, a), wh_launched("k_proj1");
+  else {
     hipLaunchKernelGGL(f, grid, block, P::LDS, st, a);
+    wh_launched("k_proj1");
+  }
   return 0;
 }
 
@@ -215,3 +219,7 @@ template int launch_proj_partial<float>(const GemmArgs&, int, hipStream_t, int*,
 template int launch_proj_partial<half_t>(const GemmArgs&, int, hipStream_t, int*, hipEvent_t, hipEvent_t);
 
 }  // namespace wh
+
+#if WH_TUNING
+WH_CT_READER(proj)
+#endif

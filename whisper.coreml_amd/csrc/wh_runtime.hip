@@ -25,6 +25,7 @@
 using namespace wh;
 
 static thread_local std::string g_err;
+static thread_local std::string g_release_error;  // a failed release in the last context destroy
 static int fail(int code, const std::string& msg) {
   g_err = msg;
   return code;
@@ -35,6 +36,22 @@ static int fail(int code, const std::string& msg) {
     hipError_t e_ = (expr);                                                                           \
     if (e_ != hipSuccess) return fail(-100, std::string(#expr) + ": " + hipGetErrorString(e_));       \
   } while (0)
+
+// A launch error (or any HIP error left pending) surfaces at the next hipGetLastError():
+// report it with the launch that raised it (tuning build: wh_launched checked every launch)
+// or, in the shipped build, the last launch before the check (wh_common.h)
+static int launch_status(const char* where) {
+  const hipError_t e = hipGetLastError();
+  std::string& first = wh_first_launch_error();
+  if (e == hipSuccess && first.empty()) return 0;
+  std::string msg = std::string(where) + ": ";
+  if (!first.empty()) msg += first;
+  else msg += std::string(hipGetErrorString(e)) + " (raised at or before the launch of " + wh_last_launch() + ")";
+  first.clear();
+  return fail(-100, msg);
+}
+
+static int enter(wh_ctx* ctx, const char* entry);
 
 #define TRY(expr)                  \
   do {                             \
@@ -133,6 +150,10 @@ struct wh_ctx {
   // tuning builds only (wh_tune_share_weights): read the weights of another context of the
   // same dims and dtype instead of this one's (probes of two window groups, one weight copy)
   virtual int share_weights_from(wh_ctx* src) = 0;
+  // weight sharing (tuning builds): the contexts reading this one's weights, and the
+  // context this one reads from; wh_destroy refuses a context others still read from
+  int sharers = 0;
+  wh_ctx* shares_from = nullptr;
   std::vector<float> token_ms;  // per-token wall ms of each decode_steps chunk
   double stats[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   int maxc = 5;
@@ -238,22 +259,35 @@ struct Ctx : public wh_ctx {
     enc = src->enc;
     dec = src->dec;
     finalized = true;
+    if (shares_from) --shares_from->sharers;
+    shares_from = src;
+    ++src->sharers;  // src's weight arena must outlive this context (wh_destroy checks)
     return 0;
   }
 
+  // every release checked: the first failure is kept (release_error) and reported by
+  // wh_destroy instead of staying pending for the next context's first call
+  std::string release_error;
+  void rel(hipError_t e, const char* what) {
+    if (e != hipSuccess && release_error.empty()) release_error = std::string(what) + ": " + hipGetErrorString(e);
+  }
   ~Ctx() override {
-    if (gexec) hipGraphExecDestroy(gexec);
-    if (graph) hipGraphDestroy(graph);
-    if (st) hipStreamDestroy(st);
-    if (wbase) hipFree(wbase);
-    if (abase) hipFree(abase);
-    if (d_audio) hipFree(d_audio);
-    if (d_mel) hipFree(d_mel);
-    for (auto& kv : d_filters) hipFree(kv.second);
-    if (d_gmax) hipFree(d_gmax);
-    if (h_done) hipHostFree(h_done);
+    if (st) rel(hipStreamSynchronize(st), "hipStreamSynchronize");
+    if (gexec) rel(hipGraphExecDestroy(gexec), "hipGraphExecDestroy");
+    if (graph) rel(hipGraphDestroy(graph), "hipGraphDestroy");
+    if (st) rel(hipStreamDestroy(st), "hipStreamDestroy");
+    if (wbase) rel(hipFree(wbase), "hipFree(weights)");
+    if (abase) rel(hipFree(abase), "hipFree(activations)");
+    if (d_audio) rel(hipFree(d_audio), "hipFree(audio)");
+    if (d_mel) rel(hipFree(d_mel), "hipFree(mel)");
+    for (auto& kv : d_filters) rel(hipFree(kv.second), "hipFree(mel filters)");
+    if (d_gmax) rel(hipFree(d_gmax), "hipFree(mel max)");
+    if (scratch) rel(hipFree(scratch), "hipFree(scratch)");
+    if (h_done) rel(hipHostFree(h_done), "hipHostFree(done flags)");
     for (auto& e : poll_ev)
-      if (e) hipEventDestroy(e);
+      if (e) rel(hipEventDestroy(e), "hipEventDestroy(poll)");
+    (void)hipGetLastError();  // what failed above is in release_error, not left pending
+    if (!release_error.empty()) g_release_error = release_error;
   }
 
   int init(int device_, const wh_dims& dims, int Wcap_, int Gcap_) {
@@ -549,7 +583,8 @@ struct Ctx : public wh_ctx {
   int64_t audio_n = 0;
   int audio_upload(const float* audio, int64_t n) override {
     if ((size_t)n > audio_cap) {
-      if (d_audio) hipFree(d_audio);
+      if (d_audio) HIPCHK(hipFree(d_audio));
+      d_audio = nullptr;
       audio_cap = std::max<size_t>(n, 16000);
       HIPCHK(hipMalloc(&d_audio, audio_cap * 4));
     }
@@ -577,17 +612,19 @@ struct Ctx : public wh_ctx {
     if (count < 0) count = total - frame0;
     if (frame0 < 0 || count < 1 || frame0 + count > total) return fail(-7, "mel frame range out of bounds");
     if (audio && (size_t)n > audio_cap) {
-      if (d_audio) hipFree(d_audio);
+      if (d_audio) HIPCHK(hipFree(d_audio));
+      d_audio = nullptr;
       audio_cap = std::max<size_t>(n, 16000);
       HIPCHK(hipMalloc(&d_audio, audio_cap * 4));
     }
     const size_t need = (size_t)n_mels * count;
     if (need > mel_cap) {
-      if (d_mel) hipFree(d_mel);
+      if (d_mel) HIPCHK(hipFree(d_mel));
+      d_mel = nullptr;
       mel_cap = need;
       HIPCHK(hipMalloc(&d_mel, mel_cap * 4));
     }
-    hipEventRecord(tm.a, st);
+    HIPCHK(hipEventRecord(tm.a, st));
     if (audio) {
       HIPCHK(hipMemcpyAsync(d_audio, audio, n * 4, hipMemcpyHostToDevice, st));
       audio_n = n;
@@ -595,10 +632,10 @@ struct Ctx : public wh_ctx {
     HIPCHK(hipMemsetAsync(d_gmax, 0, 16, st));
     launch_mel(d_audio, n, n + pad, frame0, count, d_filters[n_mels], n_mels, d_mel, count, d_gmax, st);
     if (normalize) launch_mel_norm(d_mel, count, count, n_mels, d_gmax, nullptr, st);
-    hipEventRecord(tm.b, st);
+    HIPCHK(hipEventRecord(tm.b, st));
     HIPCHK(hipStreamSynchronize(st));
     float ms = 0;
-    hipEventElapsedTime(&ms, tm.a, tm.b);
+    HIPCHK(hipEventElapsedTime(&ms, tm.a, tm.b));
     stats[0] += ms;
     mel_frames = count;
     mel_f0 = frame0;
@@ -629,7 +666,8 @@ struct Ctx : public wh_ctx {
   int mel_write(const float* mel, int64_t nf) override {
     const size_t need = (size_t)nm * nf;
     if (need > mel_cap) {
-      if (d_mel) hipFree(d_mel);
+      if (d_mel) HIPCHK(hipFree(d_mel));
+      d_mel = nullptr;
       mel_cap = need;
       HIPCHK(hipMalloc(&d_mel, mel_cap * 4));
     }
@@ -708,18 +746,18 @@ struct Ctx : public wh_ctx {
       if (s < 0 || segs[i] < 1 || s + std::min(segs[i], 3000) > mel_frames) return fail(-9, "bad window");
       h_seeks[i] = s;
     }
-    hipEventRecord(tm.a, st);
+    HIPCHK(hipEventRecord(tm.a, st));
     HIPCHK(hipMemcpyAsync(d_seeks, h_seeks.data(), n_win * 8, hipMemcpyHostToDevice, st));
     HIPCHK(hipMemcpyAsync(d_segs, segs, n_win * 4, hipMemcpyHostToDevice, st));
     const int WE = std::min(Wcap, enc_chunk());
     for (int s0 = 0; s0 < n_win; s0 += WE) TRY(encode_chunk(s0, std::min(WE, n_win - s0), n_win == 1));
-    hipEventRecord(tm.b, st);
+    HIPCHK(hipEventRecord(tm.b, st));
     HIPCHK(hipStreamSynchronize(st));
     float ms = 0;
-    hipEventElapsedTime(&ms, tm.a, tm.b);
+    HIPCHK(hipEventElapsedTime(&ms, tm.a, tm.b));
     stats[1] += ms;
     stats[5] += n_win;
-    HIPCHK(hipGetLastError());
+    TRY(launch_status(__func__));
     return 0;
   }
 
@@ -957,7 +995,11 @@ struct Ctx : public wh_ctx {
   std::string step_kernels(int n_win, int group) const override {
     const bool p1 = p1_active(n_win * group, n_win), h = sizeof(T) == 2;
     return std::string("proj=") + (p1 ? "k_proj1" : "k_proj") + ",xattn=k_xattn_seg" +
-           ",self_attn=" + (p1 ? "k_self_attn" : h && group >= 2 ? "k_self_attn_grp" : "k_self_attn_qkv") +
+           ",self_attn=" +
+           (p1 ? "k_self_attn"
+               : h && group >= 2 && self_attn_grp_mode() ? "k_self_attn_grp"
+                                                           : h && self_attn_pipe_on() ? "k_self_attn_qkv<pipe>"
+                                                                                      : "k_self_attn_qkv") +
            ",tail=" + (p1 && h && ns == 1280 && vocab_select_on() ? "k_vocab_sel" : "vocab+k_logit_part");
   }
 
@@ -1206,7 +1248,7 @@ struct Ctx : public wh_ctx {
     if (!finalized) return fail(-9, "weights not finalized");
     if (n_win < 1 || n_win > Wcap) return fail(-11, "n_win out of range");
     TRY(set_opts(o));
-    hipEventRecord(tm.a, st);
+    HIPCHK(hipEventRecord(tm.a, st));
     TRY(begin_batch(n_win, o->group, init, n_init, max_init, sot_index, o->no_speech, slots));
     S.maxc = std::max(maxc, 1);
     maxc_stride = S.maxc;
@@ -1214,15 +1256,22 @@ struct Ctx : public wh_ctx {
     // first update on the prefill logits (decoding.py:713-733, i == 0); the merge also
     // embeds each row's new token: the first step's input rows
     launch_select_merge(logits, V, S, O, n_win, st, merge_embed());
-    hipEventRecord(tm.b, st);
+    rows_dirty = false;
+    HIPCHK(hipEventRecord(tm.b, st));
     HIPCHK(hipStreamSynchronize(st));
-    HIPCHK(hipGetLastError());
+    TRY(launch_status(__func__));
     float ms = 0;
-    hipEventElapsedTime(&ms, tm.a, tm.b);
+    HIPCHK(hipEventElapsedTime(&ms, tm.a, tm.b));
     stats[2] += ms;
     return 0;
   }
 
+  // The device loop's step input rows (x_d, row_pos) are written by the previous update's
+  // merge (no k_embed per token).  Any other use of those buffers between two
+  // decode_steps calls (a first pass for alignment or prefill logits, a timing stage)
+  // sets rows_dirty, and the next decode_steps re-embeds every row once from the decode
+  // state (S.hist, S.len) before its first step.
+  bool rows_dirty = false;
   // k_merge writes the next step's input rows (x_d, row_pos): no k_embed launch per token
   MergeEmbed merge_embed() const {
     MergeEmbed em;
@@ -1258,15 +1307,15 @@ struct Ctx : public wh_ctx {
   bool step_api = false;
   int step_prefill(int n_win, int G, const int* init, const int* n_init, int max_init, const int* sot_index,
                    float* lg) override {
-    hipEventRecord(tm.a, st);
+    HIPCHK(hipEventRecord(tm.a, st));
     TRY(begin_batch(n_win, G, init, n_init, max_init, sot_index, -1));
     step_api = true;
     if (lg) HIPCHK(hipMemcpyAsync(lg, logits2, (size_t)2 * n_win * V * 4, hipMemcpyDeviceToHost, st));
-    hipEventRecord(tm.b, st);
+    HIPCHK(hipEventRecord(tm.b, st));
     HIPCHK(hipStreamSynchronize(st));
-    HIPCHK(hipGetLastError());
+    TRY(launch_status(__func__));
     float ms = 0;
-    hipEventElapsedTime(&ms, tm.a, tm.b);
+    HIPCHK(hipEventElapsedTime(&ms, tm.a, tm.b));
     stats[2] += ms;
     return 0;
   }
@@ -1282,7 +1331,7 @@ struct Ctx : public wh_ctx {
         return fail(-13, "text_offset " + std::to_string(offsets[w]) + " of window " + std::to_string(w) +
                              " != cached length " + std::to_string(h_len[w]));
     }
-    hipEventRecord(tm.a, st);
+    HIPCHK(hipEventRecord(tm.a, st));
     HIPCHK(hipMemcpyAsync(rows_in, tok, R * 4, hipMemcpyHostToDevice, st));
     launch_append_tokens(S, rows_in, cur_nwin, st);
     launch_embed<T>(E, Pdec, ns, nullptr, row_pos, S.hist, S.len, cur_G, HCTX, CTX - 1, x_d, R, st);
@@ -1290,12 +1339,12 @@ struct Ctx : public wh_ctx {
                    nullptr, nullptr, 0, true));
     TRY(vocab(nullptr, R, logits));
     if (lg) HIPCHK(hipMemcpyAsync(lg, logits, (size_t)R * V * 4, hipMemcpyDeviceToHost, st));
-    hipEventRecord(tm.b, st);
+    HIPCHK(hipEventRecord(tm.b, st));
     HIPCHK(hipStreamSynchronize(st));  // the host token buffer must outlive its copy
-    HIPCHK(hipGetLastError());
+    TRY(launch_status(__func__));
     for (auto& l : h_len) ++l;
     float ms = 0;
-    hipEventElapsedTime(&ms, tm.a, tm.b);
+    HIPCHK(hipEventElapsedTime(&ms, tm.a, tm.b));
     stats[3] += ms;
     stats[4] += 1;
     return 0;
@@ -1311,7 +1360,7 @@ struct Ctx : public wh_ctx {
     HIPCHK(hipMemcpyAsync(src_rows, src, R * 4, hipMemcpyHostToDevice, st));
     launch_reorder_rows(S, src_rows, cur_nwin, st);
     HIPCHK(hipStreamSynchronize(st));
-    HIPCHK(hipGetLastError());
+    TRY(launch_status(__func__));
     return 0;
   }
 
@@ -1359,7 +1408,11 @@ struct Ctx : public wh_ctx {
     if (cur_nwin < 1) return fail(-13, "no decode in progress");
     if (step_api) return fail(-13, "the batch was begun with wh_prefill (per-step mode): use wh_step");
     if (!eager()) TRY(ensure_graph());
-    hipEventRecord(tm.a, st);
+    HIPCHK(hipEventRecord(tm.a, st));
+    if (rows_dirty) {
+      launch_embed<T>(E, Pdec, ns, nullptr, row_pos, S.hist, S.len, cur_G, HCTX, CTX - 1, x_d, cur_nwin * cur_G, st);
+      rows_dirty = false;
+    }
     int steps = 0, done = 0;
     static const int chunk = [] {  // WHISPER_HIP_POLL_CHUNK: steps per done-flag poll (A/B)
       const char* e = tune_env("WHISPER_HIP_POLL_CHUNK");
@@ -1396,10 +1449,10 @@ struct Ctx : public wh_ctx {
       if (done == cur_nwin || kq[nb] == 0) break;
       b = nb;
     }
-    hipEventRecord(tm.b, st);
+    HIPCHK(hipEventRecord(tm.b, st));
     HIPCHK(hipStreamSynchronize(st));
     float ms = 0;
-    hipEventElapsedTime(&ms, tm.a, tm.b);
+    HIPCHK(hipEventElapsedTime(&ms, tm.a, tm.b));
     stats[3] += ms;
     stats[4] += steps;
     *n_done = done;
@@ -1433,6 +1486,7 @@ struct Ctx : public wh_ctx {
   int first_pass(int slot, const int* tokens, int n, const int* ah, int na, float* d_aqk,
                  std::vector<std::vector<int>>& keep) {
     if (!finalized) return fail(-9, "weights not finalized");
+    rows_dirty = true;  // the first pass runs its rows through x_d / row_pos
     if (slot < 0 || slot >= Wcap || n < 1 || n > CTX) return fail(-15, "bad slot or token count");
     for (int i = 0; i < n; ++i)
       if (tokens[i] < 0 || tokens[i] >= V) return fail(-15, "token out of vocabulary");
@@ -1466,7 +1520,7 @@ struct Ctx : public wh_ctx {
   int ensure_scratch(size_t bytes) {
     if (bytes <= scratch_cap) return 0;
     HIPCHK(hipStreamSynchronize(st));
-    if (scratch) hipFree(scratch);
+    if (scratch) HIPCHK(hipFree(scratch));
     scratch = nullptr;
     scratch_cap = 0;
     HIPCHK(hipMalloc((void**)&scratch, bytes));
@@ -1591,7 +1645,7 @@ struct Ctx : public wh_ctx {
     HIPCHK(hipMemcpyAsync(plens, d_plen, n_win * 4, hipMemcpyDeviceToHost, st));
     HIPCHK(hipMemcpyAsync(paths, d_path, path_off[n_win] * 4, hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
-    HIPCHK(hipGetLastError());
+    TRY(launch_status(__func__));
     return 0;
   }
 
@@ -1621,7 +1675,7 @@ struct Ctx : public wh_ctx {
     HIPCHK(hipMemcpyAsync(plen, d_plen, 4, hipMemcpyDeviceToHost, st));
     HIPCHK(hipMemcpyAsync(path, d_path, (size_t)2 * (N + M) * 4, hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
-    HIPCHK(hipGetLastError());
+    TRY(launch_status(__func__));
     return 0;
   }
 
@@ -1643,26 +1697,27 @@ struct Ctx : public wh_ctx {
     if (!rc && hipMemcpyAsync(lg, out, (size_t)n * V * 4, hipMemcpyDeviceToHost, st) != hipSuccess) rc = -100;
     if (!rc && d_aqk && hipMemcpyAsync(aqk, d_aqk, (size_t)na * n * 1500 * 4, hipMemcpyDeviceToHost, st) != hipSuccess)
       rc = -100;
-    hipStreamSynchronize(st);
-    hipFree(out);
-    if (d_aqk) hipFree(d_aqk);
-    if (rc == -100) return fail(-100, "prefill_logits: HIP copy failed");
+    if (hipStreamSynchronize(st) != hipSuccess && !rc) rc = -100;
+    if (hipFree(out) != hipSuccess && !rc) rc = -100;
+    if (d_aqk && hipFree(d_aqk) != hipSuccess && !rc) rc = -100;
+    if (rc == -100) return fail(-100, "prefill_logits: HIP copy / sync / free failed");
     if (rc) return rc;
-    HIPCHK(hipGetLastError());
+    TRY(launch_status(__func__));
     return 0;
   }
 
   int time_stage(int what, int iters, double* ms) override {
+    if (what != 0 && what != 7) rows_dirty = true;  // stages other than whole steps reuse x_d
     if (what == 0) {
       if (cur_nwin < 1) return fail(-16, "no decode batch");
       if (!eager()) TRY(ensure_graph());
-      hipEventRecord(tm.a, st);
+      HIPCHK(hipEventRecord(tm.a, st));
       for (int i = 0; i < iters; ++i) TRY(launch_step());
-      hipEventRecord(tm.b, st);
+      HIPCHK(hipEventRecord(tm.b, st));
     } else if (what == 1) {
-      hipEventRecord(tm.a, st);
+      HIPCHK(hipEventRecord(tm.a, st));
       for (int i = 0; i < iters; ++i) TRY(encode_chunk(0, 1, true));
-      hipEventRecord(tm.b, st);
+      HIPCHK(hipEventRecord(tm.b, st));
     } else if (what == 2 || what == 3 || what == 5 || what == 6) {
       // per-launch time of one decoder-step kernel at the current batch, over all
       // layers (so weights / cross-KV stream from HBM as in the step, not from cache):
@@ -1675,7 +1730,7 @@ struct Ctx : public wh_ctx {
       const int nl = warm ? 1 : Ld;
       const int R = cur_nwin * cur_G, n = ns;
       int launches = 0;
-      hipEventRecord(tm.a, st);
+      HIPCHK(hipEventRecord(tm.a, st));
       for (int i = 0; i < iters * (warm ? Ld : 1); ++i)
         for (int l = 0; l < nl; ++l) {
           auto& e = dec[l];
@@ -1691,10 +1746,10 @@ struct Ctx : public wh_ctx {
             ++launches;
           }
         }
-      hipEventRecord(tm.b, st);
+      HIPCHK(hipEventRecord(tm.b, st));
       HIPCHK(hipStreamSynchronize(st));
       float t = 0;
-      hipEventElapsedTime(&t, tm.a, tm.b);
+      HIPCHK(hipEventElapsedTime(&t, tm.a, tm.b));
       *ms = t / launches;
       return 0;
     } else if (what == 7) {
@@ -1716,11 +1771,13 @@ struct Ctx : public wh_ctx {
       if (rc == 0 && hipStreamSynchronize(st) != hipSuccess) rc = fail(-100, "time_stage(7): sync failed");
       for (int j = 0; rc == 0 && j < proj_ev_n; ++j) {
         float t = 0;
-        hipEventElapsedTime(&t, proj_ev[2 * j], proj_ev[2 * j + 1]);
+        if (hipEventElapsedTime(&t, proj_ev[2 * j], proj_ev[2 * j + 1]) != hipSuccess)
+          rc = fail(-100, "time_stage(7): hipEventElapsedTime failed");
         tot += t;
         ++launches;
       }
-      for (auto& ev : proj_ev) hipEventDestroy(ev);
+      for (auto& ev : proj_ev)
+        if (hipEventDestroy(ev) != hipSuccess && rc == 0) rc = fail(-100, "time_stage(7): hipEventDestroy failed");
       proj_ev.clear();
       proj_ev_n = 0;
       if (rc) return rc;
@@ -1729,15 +1786,15 @@ struct Ctx : public wh_ctx {
     } else if (what == 4) {
       // the token-selection kernel alone on the current logits (state unchanged)
       if (cur_nwin < 1) return fail(-16, "no decode batch");
-      hipEventRecord(tm.a, st);
+      HIPCHK(hipEventRecord(tm.a, st));
       for (int i = 0; i < iters; ++i) launch_logit_rows(logits, V, S, O, cur_nwin, st);
-      hipEventRecord(tm.b, st);
+      HIPCHK(hipEventRecord(tm.b, st));
     } else {
       return fail(-2, "time_stage: unknown stage");
     }
     HIPCHK(hipStreamSynchronize(st));
     float t = 0;
-    hipEventElapsedTime(&t, tm.a, tm.b);
+    HIPCHK(hipEventElapsedTime(&t, tm.a, tm.b));
     *ms = t / iters;
     return 0;
   }
@@ -1775,13 +1832,21 @@ int wh_create(int device, const wh_dims* dims, int compute_dtype, int max_window
 }
 
 int wh_destroy(wh_ctx* ctx) {
+  if (!ctx) return 0;
+  if (ctx->sharers > 0)
+    return fail(-1, "wh_destroy: " + std::to_string(ctx->sharers) +
+                        " context(s) still read this context's weights (wh_tune_share_weights): destroy them first");
+  if (ctx->shares_from) --ctx->shares_from->sharers;
+  hipSetDevice(ctx->device);
+  g_release_error.clear();
   delete ctx;
+  if (!g_release_error.empty()) return fail(-100, "wh_destroy: " + g_release_error);
   return 0;
 }
 
 int wh_set_mel_filters(wh_ctx* ctx, int n_mels, const float* filters) {
   if (!ctx || !filters) return fail(-1, "null argument");
-  hipSetDevice(ctx->device);
+  if (const int rc = enter(ctx, __func__)) return rc;
   std::vector<float> f(filters, filters + (size_t)n_mels * 201);
   // both element-type contexts share the filter map through the base pointer cast
   auto* c16 = dynamic_cast<Ctx<half_t>*>(ctx);
@@ -1799,11 +1864,21 @@ int wh_set_mel_filters(wh_ctx* ctx, int n_mels, const float* filters) {
   return 0;
 }
 
-#define CTXCALL(expr)                                  \
-  do {                                                 \
-    if (!ctx) return fail(-1, "null context");         \
-    hipSetDevice(ctx->device);                         \
-    return (expr);                                     \
+// every context call: on the context's device, and no HIP error pending from before it
+// (a pending one belongs to an earlier call: reported as such, not as this call's failure)
+static int enter(wh_ctx* ctx, const char* entry) {
+  if (!ctx) return fail(-1, "null context");
+  const hipError_t e = hipSetDevice(ctx->device);
+  if (e != hipSuccess) return fail(-100, std::string(entry) + ": hipSetDevice: " + hipGetErrorString(e));
+  const int rc = launch_status("HIP error pending before this call");
+  if (rc) g_err = std::string(entry) + ": " + g_err;
+  return rc;
+}
+#define CTXCALL(expr)                            \
+  do {                                           \
+    const int rc_e = enter(ctx, __func__);       \
+    if (rc_e) return rc_e;                       \
+    return (expr);                               \
   } while (0)
 
 int wh_load_tensor(wh_ctx* ctx, const char* name, const float* data, const int64_t* shape, int ndim) {
@@ -1898,10 +1973,10 @@ int wh_step_kernels(wh_ctx* ctx, int n_win, int group, char* buf, int cap) {
   return n;
 }
 int wh_sync(wh_ctx* ctx) {
-  if (!ctx) return fail(-1, "null context");
-  hipSetDevice(ctx->device);
+  const int rc = enter(ctx, __func__);
+  if (rc) return rc;
   HIPCHK(hipDeviceSynchronize());
-  return 0;
+  return launch_status(__func__);
 }
 int wh_time_stage(wh_ctx* ctx, int what, int iters, double* ms) { CTXCALL(ctx->time_stage(what, iters, ms)); }
 #if WH_TUNING

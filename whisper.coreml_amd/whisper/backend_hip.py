@@ -168,13 +168,18 @@ class HipContext:
             raise HipBackendError(f"{what} failed ({rc}): {msg}")
 
     def close(self):
+        """Release the context; raises HipBackendError if a HIP release failed (wh_destroy
+        reports it instead of leaving the error pending for the next context)."""
         if getattr(self, "h", None):
-            self.lib.wh_destroy(self.h)
-            self.h = None
+            h, self.h = self.h, None
+            self._check(self.lib.wh_destroy(h), "wh_destroy")
 
     def __del__(self):
         try:
             self.close()
+        except HipBackendError as e:  # no raising from a finalizer: report it
+            import warnings
+            warnings.warn(str(e), RuntimeWarning)
         except Exception:
             pass
 
