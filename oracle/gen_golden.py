@@ -605,6 +605,44 @@ def dtw_goldens():
     print("dtw goldens:", len(out))
 
 
+def checkpoint_goldens(name: str = "micro", seed: int = 0, audio_seed: int = 1):
+    """A checkpoint in the released format (VERDICT r04 item 8): {"dims", "model_state_dict"}
+    from the reference's own Whisper.state_dict() on the seeded weights, every tensor fp16
+    as OpenAI's released .pt files store them, written with torch.save to
+    tests/golden/<name>_ckpt.pt; then the REFERENCE's load_model(path) (__init__.py:151-166)
+    loads it back and decodes a seeded 30 s window (fp32 CPU path): greedy and beam 5 with
+    EOT suppressed (224 steps of fixed work) and natural greedy.  Tokens / avg_logprob go
+    to tests/golden/<name>_ckpt.json with the checkpoint's sha256."""
+    import hashlib
+    model, _ = build_ref_model(name, seed)
+    dims = syn.MODEL_DIMS[name]
+    state = {k: v.detach().half().contiguous() for k, v in model.state_dict().items()}
+    path = os.path.join(OUT, f"{name}_ckpt.pt")
+    torch.save({"dims": dict(dims), "model_state_dict": state}, path)
+    del model
+    ref = refw.load_model(path, device="cpu")
+    ref.eval()
+    tok = ref_tok.get_tokenizer(ref.is_multilingual, num_languages=ref.num_languages, language="en",
+                                task="transcribe")
+    audio = syn.synthetic_audio(30.0, seed=audio_seed)
+    mel = ref_audio.log_mel_spectrogram(audio, dims["n_mels"], padding=N_SAMPLES)
+    seg = ref_audio.pad_or_trim(mel[:, :3000], 3000)
+    cases = {"greedy_fixed": dict(suppress_tokens=f"-1,{tok.eot}"),
+             "beam_fixed": dict(beam_size=5, suppress_tokens=f"-1,{tok.eot}"),
+             "greedy_natural": {}}
+    out = {}
+    for key, kw in cases.items():
+        r = refw.decode(ref, seg, ref_decoding.DecodingOptions(temperature=0.0, language="en", fp16=False, **kw))
+        out[key] = dict(options=kw, tokens=[int(t) for t in r.tokens], avg_logprob=float(r.avg_logprob),
+                        no_speech_prob=float(r.no_speech_prob))
+        print(f"[{name} checkpoint] {key}: {len(r.tokens)} tokens, avg_logprob {r.avg_logprob:.5f}", flush=True)
+    with open(path, "rb") as f:
+        sha = hashlib.sha256(f.read()).hexdigest()
+    with open(os.path.join(OUT, f"{name}_ckpt.json"), "w") as f:
+        json.dump(dict(checkpoint=os.path.basename(path), sha256=sha, dims=dims, seed=seed, audio_seed=audio_seed,
+                       state_dtype="float16", keys=sorted(state), cases=out), f, indent=0)
+
+
 def asset_export():
     """Product asset (data only): language codes in token order and, per
     vocabulary, the special ids / SuppressTokens(-1) list / whitespace-only ids
@@ -644,6 +682,8 @@ def main(argv):
             prefix_goldens()
         elif w == "beam_options":
             beam_option_goldens()
+        elif w.endswith("_ckpt"):
+            checkpoint_goldens(w[:-len("_ckpt")])
         elif w.endswith("_steps_mixed"):
             step_goldens_mixed(w[:-len("_steps_mixed")])
         elif w.endswith("_words_beam"):

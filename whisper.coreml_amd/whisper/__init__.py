@@ -87,8 +87,16 @@ def load_model(name: str, device: Optional[Union[str, int]] = None, download_roo
     else:
         raise RuntimeError(f"Model {name} not found; available models = {available_models()}")
     if ckpt is not None:
+        import io
         import torch
-        checkpoint = torch.load(ckpt, map_location="cpu", weights_only=True)
+        # the reference's loader (__init__.py:151-166): a released checkpoint is a torch.save'd
+        # {"dims": dict, "model_state_dict": fp16 tensors}; loaded with weights_only=True (no
+        # pickled code runs), optionally from bytes read up front (in_memory)
+        if in_memory:
+            with open(ckpt, "rb") as f:
+                checkpoint = torch.load(io.BytesIO(f.read()), map_location="cpu", weights_only=True)
+        else:
+            checkpoint = torch.load(ckpt, map_location="cpu", weights_only=True)
         dims = ModelDimensions(**checkpoint["dims"])
         state = checkpoint["model_state_dict"]
     else:
