@@ -151,7 +151,10 @@ int wh_reorder_kv(wh_ctx* ctx, const int* source_rows);
 /* decoder forward over tokens at offset 0 for one window slot (Whisper.forward,
    model.py:110-119 / the decoder256 first pass); logits [n_tokens][n_vocab];
    align_qk (nullable) [n_align][n_tokens][n_audio_ctx] raw cross q.k of the heads
-   in align_heads (layer*n_head + head) */
+   in align_heads (layer*n_head + head).  Like the reference's first pass, it writes the
+   slot's self-KV rows: call it (and wh_align / wh_align_batch) on a slot whose decode has
+   finished or that is not in the current batch; a device-loop decode of OTHER slots may
+   continue with wh_decode_steps afterwards (its step rows are re-embedded first). */
 int wh_prefill_logits(wh_ctx* ctx, int slot, const int* tokens, int n_tokens, float* logits, const int* align_heads,
                       int n_align, float* align_qk);
 

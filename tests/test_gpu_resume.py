@@ -7,7 +7,10 @@ timing stage — must not change the decode: the next chunk re-embeds every row 
 decode state first (wh_runtime.hip rows_dirty).  Checked on the micro model in fp32: a
 decode of three windows (split-K k_proj layers) and of one window (k_proj1 layers) cut
 into chunks with alignment / prefill work between them gives exactly the tokens,
-log-probabilities and candidates of the same decode run in one call."""
+log-probabilities and candidates of the same decode run in one call.  The interleaved first
+passes use encoder slot 3, outside the decode batch: a first pass writes its window slot's
+self-KV rows (as the reference's alignment pass does after that window's decode), so it
+may run on a finished or idle slot, not on one still decoding."""
 import numpy as np
 import pytest
 
@@ -28,12 +31,12 @@ def _setup(m, n):
     from whisper.audio import N_FRAMES
     from whisper.decoding import DecodingTask
     mels = []
-    for s in range(n):
+    for s in range(4):
         audio = S.synthetic_audio(30.0, seed=700 + s)
         mel = whisper.log_mel_spectrogram(audio, m.dims.n_mels, padding=whisper.audio.N_SAMPLES)
         mels.append(whisper.pad_or_trim(mel[:, :3000], 3000))
     m.ctx.mel_write(np.concatenate(mels, axis=1))
-    m.ctx.encode([i * N_FRAMES for i in range(n)], [N_FRAMES] * n)
+    m.ctx.encode([i * N_FRAMES for i in range(4)], [N_FRAMES] * 4)  # slots 0..3
     # fixed work (EOT suppressed: no early stop) so every chunk boundary falls inside a
     # live decode
     from whisper.tokenizer import get_tokenizer
@@ -68,9 +71,9 @@ def test_decode_resumes_after_alignment_and_prefill(micro32, n):
     m.ctx.decode_begin(task.wh_opts(), init, [task.sot_index] * n)
     done = m.ctx.decode_steps(9)
     assert done < n, "the decode must still be live at the first cut"
-    m.ctx.align_batch([0], [seq], len(tok.sot_sequence), [3000], heads)   # a first pass through x_d
+    m.ctx.align_batch([3], [seq], len(tok.sot_sequence), [3000], heads)   # a first pass through x_d
     m.ctx.decode_steps(17)
-    m.ctx.prefill_logits(n - 1, list(task.initial_tokens) + list(range(200, 230)))  # another one
+    m.ctx.prefill_logits(3, list(task.initial_tokens) + list(range(200, 230)))  # another one
     m.ctx.time_stage(2, 1)  # the six projections of every layer on the current rows
     m.ctx.decode_steps(task.sample_len)
     got = _read(m, task, n)

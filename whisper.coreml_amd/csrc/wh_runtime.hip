@@ -210,6 +210,7 @@ struct Ctx : public wh_ctx {
   T *xn_d, *q_d, *att_d, *hm_d;
   int *row_tok, *row_pos, *row_win, *row_slot, *win_row0, *win_nrows, *win_slot, *rows_in, *src_rows;
   int *st_row_win, *st_row_slot, *st_win_row0, *st_win_nrows, *st_win_slot;
+  int* fp_anc = nullptr;
   static constexpr int P1_SLABS = 2048;  // k_proj1 split-K slabs: zs x 16-column tiles <= 16 x 80 at n = 1280
   float* p1_slab = nullptr;  // k_proj1 in-launch split-K slabs [zs][N/16][256]
   float* vs_rec = nullptr;   // k_vocab_sel records
@@ -383,6 +384,7 @@ struct Ctx : public wh_ctx {
     addA(Wcap * 8); addA(Wcap * 4);
     // state
     addA((size_t)Wcap * Gcap * HCTX * 4); addA((size_t)Wcap * Gcap * CTX * 4);
+    addA((size_t)Wcap * CTX * 4);  // fp_anc
     for (int i = 0; i < 5; ++i) addA(Wcap * 4);
     addA(Wcap * Gcap * 4);
     addA(Wcap * 16 * 4); addA(Wcap * 16 * 4); addA((size_t)Wcap * 16 * HCTX * 4);
@@ -422,6 +424,7 @@ struct Ctx : public wh_ctx {
     suppress = (unsigned*)ia((V + 31) / 32);
     d_seeks = (int64_t*)aa.take(Wcap * 8); d_segs = ia(Wcap);
     S.hist = ia((size_t)Wcap * Gcap * HCTX); S.anc = ia((size_t)Wcap * Gcap * CTX);
+    fp_anc = ia((size_t)Wcap * CTX);  // first passes' ancestry: all zero (beam slot 0), never written
     S.len = ia(Wcap); S.sample_begin = ia(Wcap); S.step = ia(Wcap); S.done = ia(Wcap); S.fin_n = ia(Wcap);
     S.sum_lp = fa(Wcap * Gcap);
     S.fin_score = fa(Wcap * 16); S.fin_len = ia(Wcap * 16); S.fin_tok = ia((size_t)Wcap * 16 * HCTX);
@@ -434,7 +437,7 @@ struct Ctx : public wh_ctx {
     xs_rec = fa((size_t)Wcap * nh * XS_NSP * XREC); xs_cnt = ia((size_t)Wcap * nh);
     x2_d = fa((size_t)8 * n);
     ekz_slab = fa((size_t)EKZ_TILES(n) * 16384); ekz_cnt = ia((size_t)EKZ_TILES(n) * 4);  // zeroed with the arena
-    if (!S.seed || !S.cand_idx || !S.lp_cnt || !S.lpw_cnt || !vs_cnt || !p1_cnt || !xs_cnt || !x2_d || !ekz_cnt)
+    if (!fp_anc || !S.seed || !S.cand_idx || !S.lp_cnt || !S.lpw_cnt || !vs_cnt || !p1_cnt || !xs_cnt || !x2_d || !ekz_cnt)
       return fail(-3, "activation arena overflow");
     S.nw = Wcap; S.G = 1; S.ctx = CTX; S.hctx = HCTX; S.maxc = 16;
     HIPCHK(hipMalloc(&d_gmax, 64));
@@ -866,8 +869,12 @@ struct Ctx : public wh_ctx {
   // decoder LayerNorm of every row (decoder.py:316) — except on the k_proj1 path
   // (dec_layers_p1), which leaves final_x set instead: vocab() computes that LayerNorm
   // in its prologue.
+  // anc: the ancestry table the self-attention reads ([w][ancG][CTX]); the decode's S.anc
+  // unless a first pass (alignment / prefill logits) gives its own (fp_anc: all zeros)
   int dec_layers(int R, const int* rw, const int* rs, const int* rp, int ancG, int nwin, const int* wr0, const int* wnr,
-                 const int* wsl, float* aqk, const int* qkmap, int qkrows, bool step = false) {
+                 const int* wsl, float* aqk, const int* qkmap, int qkrows, bool step = false,
+                 const int* anc = nullptr) {
+    const int* A = anc ? anc : S.anc;
     const int n = ns;
     // step mode (one row per beam, rows independent): the skinny projections run
     // split-K into fp32 partial slabs; QKV's reduction is fused into self-attention
@@ -875,14 +882,14 @@ struct Ctx : public wh_ctx {
     GemmArgs g;
     final_x = nullptr;
     if (step && !qkmap && p1_active(R, nwin))
-      return dec_layers_p1(R, rw, rs, rp, ancG, nwin, wr0, wnr, wsl);
+      return dec_layers_p1(R, rw, rs, rp, ancG, nwin, wr0, wnr, wsl, A);
     launch_layernorm<T>(x_d, xn_d, dec[0].ln1_g, dec[0].ln1_b, R, n, 1e-5f, nullptr, st);
     for (int l = 0; l < Ld; ++l) {
       auto& e = dec[l];
       if (skinny) {
         int ks = 0;
         TRY(partial(xn_d, n, e.wqkv, R, 3 * n, n, &ks, false));  // k_self_attn_qkv reads fp32 slabs
-        if (launch_self_attn_qkv<T>(part, ks, (int64_t)R * 3 * n, e.bqkv, n, kc[l], vc[l], rw, rs, rp, S.anc, ancG,
+        if (launch_self_attn_qkv<T>(part, ks, (int64_t)R * 3 * n, e.bqkv, n, kc[l], vc[l], rw, rs, rp, A, ancG,
                                     Gcap, nh, CTX, att_d, n, R, st, slab_h))
           return fail(-20, "self-attention rows are not a whole number of beam groups");
       } else {
@@ -890,7 +897,7 @@ struct Ctx : public wh_ctx {
         g.out = q_d; g.ldo = n; g.hs_state = n; g.hs_heads = nh;
         g.row_win = rw; g.row_slot = rs; g.row_pos = rp; g.kc = kc[l]; g.vc = vc[l]; g.kv_beams = Gcap; g.kv_ctx = CTX;
         TRY(gemm(xn_d, n, e.wqkv, e.bqkv, R, 3 * n, n, EPI_QKV_DEC, g));
-        launch_self_attn<T>(q_d, n, kc[l], vc[l], rw, rs, rp, S.anc, ancG, Gcap, nh, CTX, att_d, n, R, st);
+        launch_self_attn<T>(q_d, n, kc[l], vc[l], rw, rs, rp, A, ancG, Gcap, nh, CTX, att_d, n, R, st);
       }
       TRY(resid(att_d, n, e.wo, e.bo, R, e.lnx_g, e.lnx_b));
       // cross-attention query: in step mode its split-K slabs are reduced inside
@@ -1004,7 +1011,7 @@ struct Ctx : public wh_ctx {
   }
 
   int dec_layers_p1(int R, const int* rw, const int* rs, const int* rp, int ancG, int nwin, const int* wr0,
-                    const int* wnr, const int* wsl) {
+                    const int* wnr, const int* wsl, const int* A) {
     const int n = ns;
     // deferred residual: fc2 stores its two K-half slabs only; the next layer's QKV
     // LayerNorm prologue adds them (+ bias) to the current rows and one of its workgroups
@@ -1038,7 +1045,7 @@ struct Ctx : public wh_ctx {
       g.row_win = rw; g.row_slot = rs; g.row_pos = rp; g.kc = kc[l]; g.vc = vc[l]; g.kv_beams = Gcap; g.kv_ctx = CTX;
       TRY(p1(g, EPI_QKV_DEC, true));
       ln_done();
-      launch_self_attn<T>(q_d, n, kc[l], vc[l], rw, rs, rp, S.anc, ancG, Gcap, nh, CTX, att_d, n, R, st);
+      launch_self_attn<T>(q_d, n, kc[l], vc[l], rw, rs, rp, A, ancG, Gcap, nh, CTX, att_d, n, R, st);
       TRY(resid(att_d, n, e.wo, e.bo, false));  // deferring it measured +1.0 us on cross-q, -0.2 here
       // cross-attention block
       g = GemmArgs();
@@ -1272,6 +1279,11 @@ struct Ctx : public wh_ctx {
   // sets rows_dirty, and the next decode_steps re-embeds every row once from the decode
   // state (S.hist, S.len) before its first step.
   bool rows_dirty = false;
+  void restore_rows() {
+    if (!rows_dirty || cur_nwin < 1 || step_api) return;
+    launch_embed<T>(E, Pdec, ns, nullptr, row_pos, S.hist, S.len, cur_G, HCTX, CTX - 1, x_d, cur_nwin * cur_G, st);
+    rows_dirty = false;
+  }
   // k_merge writes the next step's input rows (x_d, row_pos): no k_embed launch per token
   MergeEmbed merge_embed() const {
     MergeEmbed em;
@@ -1409,10 +1421,7 @@ struct Ctx : public wh_ctx {
     if (step_api) return fail(-13, "the batch was begun with wh_prefill (per-step mode): use wh_step");
     if (!eager()) TRY(ensure_graph());
     HIPCHK(hipEventRecord(tm.a, st));
-    if (rows_dirty) {
-      launch_embed<T>(E, Pdec, ns, nullptr, row_pos, S.hist, S.len, cur_G, HCTX, CTX - 1, x_d, cur_nwin * cur_G, st);
-      rows_dirty = false;
-    }
+    restore_rows();
     int steps = 0, done = 0;
     static const int chunk = [] {  // WHISPER_HIP_POLL_CHUNK: steps per done-flag poll (A/B)
       const char* e = tune_env("WHISPER_HIP_POLL_CHUNK");
@@ -1495,7 +1504,6 @@ struct Ctx : public wh_ctx {
     rt.assign(tokens, tokens + n); rp.resize(n); rw.assign(n, slot); rs.assign(n, 0);
     keep[4] = {0}; keep[5] = {n}; keep[6] = {slot};
     for (int i = 0; i < n; ++i) rp[i] = i;
-    keep[7].assign((size_t)CTX, 0);
     auto& map = keep[8];
     map.assign((size_t)Ld * nh, -1);
     for (int i = 0; i < na; ++i)
@@ -1507,11 +1515,12 @@ struct Ctx : public wh_ctx {
     HIPCHK(hipMemcpyAsync(win_row0, keep[4].data(), 4, hipMemcpyHostToDevice, st));
     HIPCHK(hipMemcpyAsync(win_nrows, keep[5].data(), 4, hipMemcpyHostToDevice, st));
     HIPCHK(hipMemcpyAsync(win_slot, keep[6].data(), 4, hipMemcpyHostToDevice, st));
-    HIPCHK(hipMemcpyAsync(S.anc + (size_t)slot * CTX, keep[7].data(), CTX * 4, hipMemcpyHostToDevice, st));
     HIPCHK(hipMemcpyAsync(qk_map, map.data(), map.size() * 4, hipMemcpyHostToDevice, st));
     launch_embed<T>(E, Pdec, ns, row_tok, row_pos, nullptr, nullptr, 1, HCTX, CTX - 1, x_d, n, st);
+    // its own all-zero ancestry table: the decode's S.anc ([w][G][CTX]) stays untouched,
+    // so a device-loop decode of other slots can continue afterwards
     return dec_layers(n, row_win, row_slot, row_pos, 1, 1, win_row0, win_nrows, win_slot, d_aqk,
-                      d_aqk ? qk_map : nullptr, n);
+                      d_aqk ? qk_map : nullptr, n, false, fp_anc);
   }
 
   // grow-only device scratch for the alignment / prefill readbacks
@@ -1589,7 +1598,6 @@ struct Ctx : public wh_ctx {
       if (ah[i] >= 0 && ah[i] < Ld * nh) map[ah[i]] = i;
     HIPCHK(hipMemcpyAsync(qk_map, map.data(), map.size() * 4, hipMemcpyHostToDevice, st));
     std::vector<DtwJob> jobs(n_win);
-    std::vector<int> anc0((size_t)CTX, 0);
     const int eot = tokens[tok_off[1] - 1];
     for (int w0 = 0; w0 < n_win;) {
       int nw = 0, R = 0;
@@ -1603,7 +1611,6 @@ struct Ctx : public wh_ctx {
         for (int q = 0; q < n; ++q, ++r) { rt[r] = tokens[tok_off[w] + q]; rp[r] = q; rw[r] = slots[w]; }
         for (int k = 0; k < n - n_sot - 2; ++k) sel.push_back(wr0[i] + n_sot + k);
         if (tokens[tok_off[w] + n - 1] != eot) return fail(-15, "align: windows must end with the same eot");
-        HIPCHK(hipMemcpyAsync(S.anc + (size_t)slots[w] * CTX, anc0.data(), CTX * 4, hipMemcpyHostToDevice, st));
       }
       for (int q = 0; q < R; ++q)
         if (rt[q] < 0 || rt[q] >= V) return fail(-15, "align: token out of vocabulary");
@@ -1614,8 +1621,10 @@ struct Ctx : public wh_ctx {
       HIPCHK(hipMemcpyAsync(win_row0, wr0.data(), nw * 4, hipMemcpyHostToDevice, st));
       HIPCHK(hipMemcpyAsync(win_nrows, wnr.data(), nw * 4, hipMemcpyHostToDevice, st));
       HIPCHK(hipMemcpyAsync(win_slot, wsl.data(), nw * 4, hipMemcpyHostToDevice, st));
+      rows_dirty = true;  // this first pass runs its rows through x_d / row_pos
       launch_embed<T>(E, Pdec, ns, row_tok, row_pos, nullptr, nullptr, 1, HCTX, CTX - 1, x_d, R, st);
-      TRY(dec_layers(R, row_win, row_slot, row_pos, 1, nw, win_row0, win_nrows, win_slot, d_qk, qk_map, R));
+      TRY(dec_layers(R, row_win, row_slot, row_pos, 1, nw, win_row0, win_nrows, win_slot, d_qk, qk_map, R, false,
+                     fp_anc));
       // probabilities of the text tokens, 128 logit rows at a time
       const int64_t pb = prob_off[w0];
       for (int c0 = 0; c0 < (int)sel.size(); c0 += 128) {
@@ -1707,7 +1716,11 @@ struct Ctx : public wh_ctx {
   }
 
   int time_stage(int what, int iters, double* ms) override {
-    if (what != 0 && what != 7) rows_dirty = true;  // stages other than whole steps reuse x_d
+    // the stages run on the live batch's step rows: restore them first (a first pass may
+    // have left its own positions in row_pos, where the projections' QKV epilogue would
+    // write the decode's self-KV); stages other than whole steps leave x_d dirty
+    restore_rows();
+    if (what != 0 && what != 7) rows_dirty = true;
     if (what == 0) {
       if (cur_nwin < 1) return fail(-16, "no decode batch");
       if (!eager()) TRY(ensure_graph());
