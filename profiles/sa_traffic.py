@@ -1,0 +1,63 @@
+"""HBM traffic of the step self-attention (k_self_attn_qkv) at late context (round 5):
+does the L2 dedupe the beams' shared history rows, or does every (row, head) wave pull its
+whole history from HBM?  Workload (`run`): large-v3 fp16, 20 windows x beam 5, eager
+steps (WHISPER_HIP_EAGER=1, tuning library: rocprofv3 follows eager dispatches) advanced
+to ~205 tokens of context; `parse <fetch dir> <write dir>` reports the LAST step's 32
+self-attention dispatches (FETCH_SIZE x 2 gfx950 read correction, WRITE_SIZE exact) beside
+the logical K/V bytes (rows x heads x 2 x t x 64 x 2 B).
+  cd /tmp && export TMPDIR=/tmp
+  WHISPER_HIP_EAGER=1 WHISPER_HIP_LIB=... rocprofv3 --pmc FETCH_SIZE --kernel-trace -d D -o run --output-format csv -- python sa_traffic.py run
+"""
+import csv
+import glob
+import json
+import os
+import sys
+from collections import defaultdict
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+STEPS = 200
+
+
+def run():
+    sys.path.insert(0, os.path.join(REPO, "whisper.coreml_amd"))
+    import whisper
+    from whisper import synthetic as S
+    from whisper.decoding import DecodingTask
+    dims = S.MODEL_DIMS["large-v3"]
+    m = whisper.Whisper(whisper.ModelDimensions(**dims), "large-v3", device=0, dtype="fp16", max_windows=20, max_group=5)
+    m.load_state_dict(S.synthetic_state_dict(dims, 0))
+    m.ctx.log_mel(S.synthetic_audio(600.0, seed=1000), dims["n_mels"], padding=480000)
+    m.ctx.encode([3000 * i for i in range(20)], [3000] * 20)
+    task = DecodingTask(m, whisper.DecodingOptions(language="en", beam_size=5))
+    m.ctx.decode_begin(task.wh_opts(), [task.initial_tokens] * 20, [task.sot_index] * 20)
+    print("step ms", m.ctx.time_stage(0, STEPS), flush=True)
+    m.close()
+
+
+def _per_dispatch(d, counter):
+    per, names = defaultdict(float), {}
+    for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+        for r in csv.DictReader(open(f)):
+            if r.get("Counter_Name") == counter:
+                k = int(r["Dispatch_Id"])
+                per[k] += float(r["Counter_Value"])
+                names[k] = r["Kernel_Name"]
+    return per, names
+
+
+def parse(dfetch, dwrite):
+    out = {}
+    for counter, d, scale in (("FETCH_SIZE", dfetch, 2 * 1024), ("WRITE_SIZE", dwrite, 1024)):
+        per, names = _per_dispatch(d, counter)
+        ids = sorted(k for k in per if "k_self_attn_qkv" in names[k])[-32:]
+        out[counter] = scale * sum(per[k] for k in ids) / max(len(ids), 1)
+        out[counter + "_dispatches"] = len(ids)
+    t = 4 + STEPS  # context positions of the traced step (sot sequence + generated)
+    out["logical_kv_bytes"] = 100 * 20 * 2 * t * 64 * 2
+    out["context"] = t
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    run() if sys.argv[1] == "run" else parse(sys.argv[2], sys.argv[3])

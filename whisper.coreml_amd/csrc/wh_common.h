@@ -76,15 +76,16 @@ inline void wh_launched(const char* name) {
 // launch (layer 31's).  Mark 0 = workgroup start, 1 / 2 = kernel-specific phase ends,
 // 3 = thread 0 done (its stores drained).  Each translation unit has its own copy of the
 // array (static) and reader (WH_CT_READER); the slots of one role live in one unit.
-constexpr int CT_SLOTS = 10, CT_WG = 2048;
+constexpr int CT_SLOTS = 11, CT_WG = 2048;
 enum { CT_PROJ_QKV = 0, CT_PROJ_NN = 1, CT_PROJ_FC1 = 2, CT_PROJ_FC2 = 3, CT_RESID_LN = 4, CT_REDUCE = 5,
-       CT_SELF_ATTN = 6, CT_XATTN = 7, CT_VOCAB = 8, CT_LOGIT = 9 };
+       CT_SELF_ATTN = 6, CT_XATTN = 7, CT_VOCAB = 8, CT_LOGIT = 9, CT_MERGE = 10 };
 #if WH_TUNING
 static __device__ unsigned long long g_ct_trace[CT_SLOTS][CT_WG][4];
 #define CT_MARK(slot, k)                                                                 \
   do {                                                                                   \
-    if (threadIdx.x == 0 && blockIdx.x < CT_WG)                                          \
-      g_ct_trace[slot][blockIdx.x][k] = __builtin_amdgcn_s_memrealtime();                \
+    const unsigned ct_b_ = blockIdx.x + blockIdx.y * gridDim.x;                          \
+    if (threadIdx.x == 0 && ct_b_ < (unsigned)CT_WG)                                     \
+      g_ct_trace[slot][ct_b_][k] = __builtin_amdgcn_s_memrealtime();                     \
   } while (0)
 #define CT_END(slot)                                       \
   do {                                                     \

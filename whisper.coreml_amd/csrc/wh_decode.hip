@@ -356,6 +356,7 @@ __device__ void merge_embed(const MergeEmbed& em, int w, int G, int pos, const i
 template <int NT, bool SC1>
 __device__ __forceinline__ void merge_window(const DecState& s, const DecOpts& o, const MergeEmbed& em, int w, int tid, MergeLds& L) {
   static_assert(NT >= MG_MAXG * KC, "one lane per candidate");
+  CT_MARK(CT_MERGE, 0);
   const int G = s.G, len = s.len[w], sb = s.sample_begin[w];
   int* hist = s.hist + (int64_t)w * G * s.hctx;
   int* anc = s.anc + (int64_t)w * G * s.ctx;
@@ -368,6 +369,7 @@ __device__ __forceinline__ void merge_window(const DecState& s, const DecOpts& o
       __syncthreads();
       merge_embed<NT>(em, w, G, pos, L.etok, tid);
     }
+    CT_END(CT_MERGE);
     return;
   }
   const auto rsv = wt_rsrc(s.cand_val), rsi = wt_rsrc(s.cand_idx);
@@ -404,6 +406,7 @@ __device__ __forceinline__ void merge_window(const DecState& s, const DecOpts& o
       __syncthreads();
       merge_embed<NT>(em, w, G, pos, L.etok, tid);
     }
+    CT_END(CT_MERGE);
     return;
   }
   // stage old histories / ancestry and gather the candidates in ONE round trip: every
@@ -448,40 +451,71 @@ __device__ __forceinline__ void merge_window(const DecState& s, const DecOpts& o
     L.csrc[tid] = first ? (G - 1) : tid / (G + 1);
   }
   __syncthreads();
+  CT_MARK(CT_MERGE, 1);  // histories, ancestry and candidates staged
   // stable descending sort by rank (ties keep insertion order), then the walk of
   // decoding.py:375-386 in closed form: the candidate at rank q is taken iff fewer
   // than G non-EOT candidates rank above it; a non-EOT one becomes beam
   // #(non-EOT above), an EOT one finished sequence #(EOT above).  One lane per
   // candidate, no serial loop.
-  for (int c0 = tid; c0 < nc; c0 += NT) {
-    const float sc = L.csc[c0];
-    int q = 0;
-    for (int c = 0; c < nc; ++c) q += (L.csc[c] > sc) || (L.csc[c] == sc && c < c0);
-    L.rk[c0] = q;
-  }
-  if (tid == 0) L.nfin_new = 0;
-  __syncthreads();
-  for (int c0 = tid; c0 < nc; c0 += NT) {
-    const int q = L.rk[c0];
-    int ne = 0, ee = 0;  // non-EOT / EOT candidates ranked above
-    for (int c = 0; c < nc; ++c)
-      if (L.rk[c] < q) {
-        if (L.ctok[c] == o.eot) ++ee;
-        else ++ne;
-      }
+  auto take = [&](int c0, int ne, int ee, float sc, int tk, int sr) {
     if (ne < G) {
-      if (L.ctok[c0] == o.eot) {
-        L.fsc[ee] = L.csc[c0];
-        L.fsrc[ee] = L.csrc[c0];
+      if (tk == o.eot) {
+        L.fsc[ee] = sc;
+        L.fsrc[ee] = sr;
         atomicAdd(&L.nfin_new, 1);
       } else {
-        L.src[ne] = L.csrc[c0];
-        L.tok[ne] = L.ctok[c0];
-        s.sum_lp[w * G + ne] = L.csc[c0];
+        L.src[ne] = sr;
+        L.tok[ne] = tk;
+        s.sum_lp[w * G + ne] = sc;
       }
+    }
+  };
+  if (tid == 0) L.nfin_new = 0;
+  if (nc <= 64) {
+    // one wave, one candidate per lane: the other lanes' scores / ranks / tokens come from
+    // registers (v_readlane with a uniform lane index), not from ~2 x nc dependent LDS
+    // broadcast reads and a barrier between the two passes (merge 4.7 -> ~1 us of the
+    // single-window tail, profiles/r05/chain_trace_w1.txt).  Same ranks, same walk.
+    if (tid < 64) {
+      const bool live = tid < nc;
+      const float sc = live ? L.csc[tid] : 0.f;
+      const int tk = live ? L.ctok[tid] : 0, sr = live ? L.csrc[tid] : 0;
+      int q = 0;
+      for (int c = 0; c < nc; ++c) {
+        const float scc = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, sc), c));
+        q += (scc > sc) || (scc == sc && c < tid);
+      }
+      int ne = 0, ee = 0;  // non-EOT / EOT candidates ranked above
+      for (int c = 0; c < nc; ++c) {
+        const int qc = __builtin_amdgcn_readlane(q, c), tc = __builtin_amdgcn_readlane(tk, c);
+        if (qc < q) {
+          if (tc == o.eot) ++ee;
+          else ++ne;
+        }
+      }
+      if (live) take(tid, ne, ee, sc, tk, sr);
+    }
+  } else {
+    for (int c0 = tid; c0 < nc; c0 += NT) {
+      const float sc = L.csc[c0];
+      int q = 0;
+      for (int c = 0; c < nc; ++c) q += (L.csc[c] > sc) || (L.csc[c] == sc && c < c0);
+      L.rk[c0] = q;
+    }
+    __syncthreads();
+    for (int c0 = tid; c0 < nc; c0 += NT) {
+      const int q = L.rk[c0];
+      int ne = 0, ee = 0;  // non-EOT / EOT candidates ranked above
+      for (int c = 0; c < nc; ++c)
+        if (L.rk[c] < q) {
+          if (L.ctok[c] == o.eot) ++ee;
+          else ++ne;
+        }
+      take(c0, ne, ee, L.csc[c0], L.ctok[c0], L.csrc[c0]);
     }
   }
   __syncthreads();
+  CT_MARK(CT_MERGE, 2);  // ranked and walked
   // new histories / ancestry
   for (int i = tid; i < G * (len + 1); i += NT) {
     const int j = i / (len + 1), p = i - j * (len + 1);
@@ -515,6 +549,7 @@ __device__ __forceinline__ void merge_window(const DecState& s, const DecOpts& o
     __syncthreads();
     merge_embed<NT>(em, w, G, pos, L.etok, tid);
   }
+  CT_END(CT_MERGE);
 }
 
 // ---------------------------------------------------------------- split selection
@@ -718,6 +753,7 @@ __global__ __launch_bounds__(LP_THREADS) WH_LP_ATTR void k_logit_part(float* __r
     if (lane == 0) ticket = __hip_atomic_fetch_add(s.lp_cnt + r, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     ticket = __shfl(ticket, 0, 64);
     if (ticket != NS - 1) return false;
+    CT_MARK(CT_LOGIT, 1);  // this workgroup combines its row
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // no instruction: keeps the loads below the add
     if (lane == 0) __hip_atomic_store(s.lp_cnt + r, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     constexpr int N4 = NS * LP_REC / 4, PER = (N4 + 63) / 64;
@@ -746,7 +782,10 @@ __global__ __launch_bounds__(LP_THREADS) WH_LP_ATTR void k_logit_part(float* __r
     if constexpr (MERGE) {
       if (wv == 0 && lane == 0) s_go = go;
       __syncthreads();
-      if (s_go) merge_window<LP_THREADS, true>(s, o, em, w, tid, mlds);
+      if (s_go) {
+        CT_MARK(CT_LOGIT, 2);  // this workgroup merges its window
+        merge_window<LP_THREADS, true>(s, o, em, w, tid, mlds);
+      }
     }
   };
   const int need = s.G + 1;

@@ -690,6 +690,7 @@ __global__ __launch_bounds__(512) void k_vocab_small(GemmArgs a) {
 // n_win == 1 batches, whose step is already its own path: DESIGN.md §2).
 template <int D>
 __global__ __launch_bounds__(512) void k_vocab1(GemmArgs a) {
+  CT_MARK(CT_VOCAB, 0);
   constexpr int KW = 8, SW = 5, K = KW * SW * 32, TMAX = 13;  // K 1280, <= 13 tiles (launcher)
   constexpr int XROW = K * 2 + 16;
   extern __shared__ __attribute__((aligned(16))) char xs1[];
@@ -779,6 +780,7 @@ __global__ __launch_bounds__(512) void k_vocab1(GemmArgs a) {
         if (n + e < a.N) wt_store1(rs, (rr * a.ldo + n + e) * 4, v[e]);
     }
   }
+  CT_END(CT_VOCAB);
 }
 
 // ============================================================ vocabulary projection, 33-112 rows
@@ -832,6 +834,7 @@ __global__ __launch_bounds__(1024) void k_vocab_2p(GemmArgs a) {
           *reinterpret_cast<const float4_t*>(reinterpret_cast<const char*>(X + (int64_t)xr * a.ldx + h * KH) + col * 16);
     }
     __syncthreads();
+    CT_MARK(CT_VOCAB, 1 + h);  // this half of the rows staged
     if (act) {
 #pragma unroll
       for (int c = 0; c < NCH; ++c) {

@@ -369,7 +369,8 @@ __global__ __launch_bounds__(64) void k_self_attn(const T* __restrict__ q, int l
                                                   const T* __restrict__ vc, const int* __restrict__ row_win,
                                                   const int* __restrict__ row_slot, const int* __restrict__ row_pos,
                                                   const int* __restrict__ anc, int anc_beams, int nbeam, int H,
-                                                  int ctx, T* __restrict__ out, int ldo) {
+                                                  int ctx, T* __restrict__ out, int ldo) {  CT_MARK(CT_SELF_ATTN, 0);
+
   __shared__ float sc[512];
   __shared__ int slot_of[512];
   const int row = blockIdx.x, h = blockIdx.y, lane = threadIdx.x;
@@ -457,6 +458,7 @@ __global__ __launch_bounds__(64) void k_self_attn(const T* __restrict__ q, int l
       store4(op, o[0] * inv, o[1] * inv, o[2] * inv, o[3] * inv);
       store4(op + 4, o[4] * inv, o[5] * inv, o[6] * inv, o[7] * inv);
     }
+    CT_END(CT_SELF_ATTN);
     return;
   }
   if constexpr (sizeof(T) == 2) {
@@ -532,6 +534,7 @@ __global__ __launch_bounds__(64) void k_self_attn(const T* __restrict__ q, int l
       store4(op, o[0] * inv, o[1] * inv, o[2] * inv, o[3] * inv);
       store4(op + 4, o[4] * inv, o[5] * inv, o[6] * inv, o[7] * inv);
     }
+    CT_END(CT_SELF_ATTN);
     return;
   }
   // scores: lane per key
@@ -596,6 +599,7 @@ __global__ __launch_bounds__(64) void k_self_attn(const T* __restrict__ q, int l
     store4(op, o[0] * inv, o[1] * inv, o[2] * inv, o[3] * inv);
     store4(op + 4, o[4] * inv, o[5] * inv, o[6] * inv, o[7] * inv);
   }
+  CT_END(CT_SELF_ATTN);
 }
 
 template <typename T>
@@ -634,7 +638,7 @@ void launch_self_attn(const T* q, int ldq, const T* kc, const T* vc, const int* 
 // the current pass is computed (two register buffers of 8 K + 8 V fragments), q read from
 // LDS: at long contexts the passes' round trips overlap instead of adding up (the step's
 // growth over the decode is those round trips, profiles/r04/self_attn_grp64_ab.txt).
-template <typename T, bool PIPE = false>
+template <typename T, int PIPE = 0>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void k_self_attn_qkv(const float* __restrict__ part, int nsplit, int64_t part_stride,
                                                       const float* __restrict__ bqkv, int ns, T* __restrict__ kc,
                                                       T* __restrict__ vc, const int* __restrict__ row_win,
@@ -739,13 +743,31 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void
     Frag<T> ka[8], va[8], kb[8], vb[8];
     if (pos > 0) load(0, ka, va);
     int p0 = 0;
-    for (; p0 + 64 < pos; p0 += 128) {
-      load(p0 + 64, kb, vb);
-      pass(p0, ka, va);
-      if (p0 + 128 < pos) load(p0 + 128, ka, va);
-      pass(p0 + 64, kb, vb);
+    if constexpr (PIPE >= 2) {
+      // two passes in flight ahead of the one computed (three register sets, <= 256
+      // VGPRs: still two waves per SIMD, every (row, head) wave resident at once); the
+      // passes are computed in the same order, so the result is bit-identical to PIPE 1
+      Frag<T> kx[8], vx[8];
+      if (pos > 64) load(64, kb, vb);
+      for (; p0 + 128 < pos; p0 += 192) {
+        load(p0 + 128, kx, vx);
+        pass(p0, ka, va);
+        if (p0 + 192 < pos) load(p0 + 192, ka, va);
+        pass(p0 + 64, kb, vb);
+        if (p0 + 256 < pos) load(p0 + 256, kb, vb);
+        pass(p0 + 128, kx, vx);
+      }
+      if (p0 < pos) pass(p0, ka, va);
+      if (p0 + 64 < pos) pass(p0 + 64, kb, vb);
+    } else {
+      for (; p0 + 64 < pos; p0 += 128) {
+        load(p0 + 64, kb, vb);
+        pass(p0, ka, va);
+        if (p0 + 128 < pos) load(p0 + 128, ka, va);
+        pass(p0 + 64, kb, vb);
+      }
+      if (p0 < pos) pass(p0, ka, va);
     }
-    if (p0 < pos) pass(p0, ka, va);
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
       o[e] = xor8_sum(o[e]);
@@ -1157,8 +1179,17 @@ int launch_self_attn_qkv(const float* part, int nsplit, int64_t part_stride, con
   const bool pipe = self_attn_pipe_on();
   if constexpr (sizeof(T) == 2) {
     if (pipe) {
-      k_self_attn_qkv<T, true><<<rows * H, 64, 0, st>>>(part, nsplit, part_stride, bqkv, ns, kc, vc, rw, rs, rp, anc,
-                                                       anc_beams, nbeam, H, ctx, out, ldo), wh_launched("k_self_attn_qkv");
+      // WHISPER_HIP_SA_DEPTH=2 (tuning): two passes in flight ahead (A/B)
+      static const int depth = [] {
+        const char* e = tune_env("WHISPER_HIP_SA_DEPTH");
+        return e && e[0] == '2' ? 2 : 1;
+      }();
+      if (depth == 2)
+        k_self_attn_qkv<T, 2><<<rows * H, 64, 0, st>>>(part, nsplit, part_stride, bqkv, ns, kc, vc, rw, rs, rp, anc,
+                                                      anc_beams, nbeam, H, ctx, out, ldo), wh_launched("k_self_attn_qkv");
+      else
+        k_self_attn_qkv<T, 1><<<rows * H, 64, 0, st>>>(part, nsplit, part_stride, bqkv, ns, kc, vc, rw, rs, rp, anc,
+                                                      anc_beams, nbeam, H, ctx, out, ldo), wh_launched("k_self_attn_qkv");
       return 0;
     }
   }

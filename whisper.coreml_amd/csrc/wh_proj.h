@@ -220,6 +220,8 @@ __global__ __launch_bounds__(64 * NSUB * KW) void k_proj1(GemmArgs a) {
   const int kb = kz * P::KC;               // this workgroup's K range [kb, kb + KC)
   const int kw0 = kb + kw * NSTEP * 32;    // this wave's
   const T* W = reinterpret_cast<const T*>(a.W);
+  const int ct_slot = a.N == a.K ? CT_PROJ_NN : a.N == 3 * a.K ? CT_PROJ_QKV : a.N == 4 * a.K ? CT_PROJ_FC1 : CT_PROJ_FC2;
+  CT_MARK(ct_slot, 0);
 
   // 1. activations (clamped addresses, no branch around a load)
   const int CH = K / 4;  // LN: float4 chunks per residual row
@@ -358,7 +360,7 @@ __global__ __launch_bounds__(64 * NSUB * KW) void k_proj1(GemmArgs a) {
     float4_t* red = reinterpret_cast<float4_t*>(xs);  // [KW-1][NSUB][64]
     if (kw > 0) red[((kw - 1) * NSUB + sub) * 64 + lane] = acc;
     __syncthreads();
-    if (kw > 0) return;
+    if (kw > 0) return;  // (thread 0 is kw 0)
 #pragma unroll
     for (int q = 1; q < KW; ++q) acc += red[((q - 1) * NSUB + sub) * 64 + lane];
   }
@@ -374,6 +376,7 @@ __global__ __launch_bounds__(64 * NSUB * KW) void k_proj1(GemmArgs a) {
     const auto rs = __builtin_amdgcn_make_buffer_rsrc(a.p1_slab, 0, 0x7fffffff, 0x00020000);
     if constexpr (DEFER) {  // row-major [2][R][N] for the next LayerNorm prologue, which sums them
       if (r < R) store4(a.p1_slab + ((int64_t)kz * R + r) * a.N + n, acc[0], acc[1], acc[2], acc[3]);
+      CT_END(ct_slot);
       return;
     }
     __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc), rs, ((kz * ntile + tile) * 256 + lane * 4) * 4,
@@ -382,7 +385,10 @@ __global__ __launch_bounds__(64 * NSUB * KW) void k_proj1(GemmArgs a) {
     int ticket = 0;
     if (lane == 0) ticket = __hip_atomic_fetch_add(a.p1_cnt + tile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     ticket = __shfl(ticket, 0, 64);
-    if (ticket != ZS - 1) return;
+    if (ticket != ZS - 1) {
+      CT_END(ct_slot);
+      return;
+    }
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // no instruction: keeps the loads below the add
     if (lane == 0) __hip_atomic_store(a.p1_cnt + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     float4_t pv[ZS];  // every slab load issued before the first add; summed in slice order
@@ -396,7 +402,10 @@ __global__ __launch_bounds__(64 * NSUB * KW) void k_proj1(GemmArgs a) {
   }
 
   // 7. epilogue: lane holds Y[r][n0 + 4g .. +3]
-  if (r >= R) return;
+  if (r >= R) {
+    CT_END(ct_slot);
+    return;
+  }
   acc += pre_b;
   if constexpr (EPI == EPI_RESID) {
     pre_x += acc;
@@ -404,6 +413,7 @@ __global__ __launch_bounds__(64 * NSUB * KW) void k_proj1(GemmArgs a) {
   } else {
     epilogue_store<T, EPI>(a, r, 0, r, n, acc);
   }
+  CT_END(ct_slot);
 }
 
 // launch_proj1 (wh_gemm.h): a.M <= P1_RMAX rows; the configuration comes from the
