@@ -519,6 +519,7 @@ __global__ __launch_bounds__(512) void k_gemv_rows(GemmArgs a) {
 // XCD), so the second group's weight reads mostly hit that XCD's L2.
 // Every output element is one row's dot product in a fixed k order: a row's logits do not
 // depend on the other rows or on the grouping (batch invariance).
+
 template <typename T, int MT>
 __global__ __launch_bounds__(512) void k_vocab_small(GemmArgs a) {
   constexpr int VC = 8;  // k-steps per chunk
@@ -649,6 +650,9 @@ __global__ __launch_bounds__(512) void k_vocab_small(GemmArgs a) {
       }
       if (jj % nch == nch - 1) {  // tile done: lane holds rows mt*16 + r, columns n0 + 4g .. +3
         const int n = (gw + nw * (jj / nch)) * 16 + 4 * g;
+        // no bias (the launcher requires none): a conditional bias load in the store loop
+        // made the compiler wait vmcnt(0) before every store
+        const float4_t bv = (float4_t){0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int mt = 0; mt < MT; ++mt) {
           const int m = m0 + mt * 16 + r;
@@ -657,12 +661,12 @@ __global__ __launch_bounds__(512) void k_vocab_small(GemmArgs a) {
             const auto rs = wt_rsrc(a.out_f32);
 #pragma unroll
             for (int e = 0; e < 4; ++e)
-              if (n + e < a.N) wt_store1(rs, (m * a.ldo + n + e) * 4, acc[mt][e] + (a.bias ? a.bias[n + e] : 0.f));
+              if (n + e < a.N) wt_store1(rs, (m * a.ldo + n + e) * 4, acc[mt][e] + bv[e]);
 #else
             float* o = a.out_f32 + (int64_t)m * a.ldo;
 #pragma unroll
             for (int e = 0; e < 4; ++e)
-              if (n + e < a.N) o[n + e] = acc[mt][e] + (a.bias ? a.bias[n + e] : 0.f);
+              if (n + e < a.N) o[n + e] = acc[mt][e] + bv[e];
 #endif
           }
           acc[mt] = (float4_t){0.f, 0.f, 0.f, 0.f};
@@ -807,6 +811,9 @@ __global__ __launch_bounds__(1024) void k_vocab_2p(GemmArgs a) {
   const int tile = t0 + wave;
   const bool act = tile < t1;
   const half_t* X = reinterpret_cast<const half_t*>(a.X);
+  // (the row gather as a wave-uniform pointer test outside the staging: a per-chunk
+  // `a.x_rows ? ..` put a vmcnt(0) before every staging load)
+  const int* const xrows = a.x_rows;
   const half_t* wrow = reinterpret_cast<const half_t*>(a.W) + (int64_t)min(tile * 16 + r, a.N - 1) * K + 8 * g;
   float4_t acc[MT];
 #pragma unroll
@@ -827,11 +834,31 @@ __global__ __launch_bounds__(1024) void k_vocab_2p(GemmArgs a) {
       for (int c = 0; c < DEPTH - 1 && c < NCH; ++c) load_chunk(h, c, wbuf[c]);
     }
     if (h) __syncthreads();  // every wave is done with the first half's rows
-    for (int c = tid; c < a.M * CPR; c += 1024) {
-      const int row = c / CPR, col = c - row * CPR;
-      const int xr = a.x_rows ? a.x_rows[row] : row;
-      *reinterpret_cast<float4_t*>(xs2 + row * XROW + col * 16) =
-          *reinterpret_cast<const float4_t*>(reinterpret_cast<const char*>(X + (int64_t)xr * a.ldx + h * KH) + col * 16);
+    if (xrows) {
+      for (int c = tid; c < a.M * CPR; c += 1024) {
+        const int row = c / CPR, col = c - row * CPR;
+        *reinterpret_cast<float4_t*>(xs2 + row * XROW + col * 16) = *reinterpret_cast<const float4_t*>(
+            reinterpret_cast<const char*>(X + (int64_t)xrows[row] * a.ldx + h * KH) + col * 16);
+      }
+    } else {
+      // every staging load of the thread issued before the first LDS write (M <= 112: <= 9
+      // chunks per thread; the loop form waited a round trip per 16 KB iteration)
+      constexpr int SU = (112 * CPR + 1023) / 1024;
+      float4_t tmp[SU];
+#pragma unroll
+      for (int u = 0; u < SU; ++u) {
+        const int c = min(tid + 1024 * u, a.M * CPR - 1), row = c / CPR, col = c - row * CPR;
+        tmp[u] = *reinterpret_cast<const float4_t*>(reinterpret_cast<const char*>(X + (int64_t)row * a.ldx + h * KH) +
+                                                    col * 16);
+      }
+#pragma unroll
+      for (int u = 0; u < SU; ++u) {
+        const int c = tid + 1024 * u;
+        if (c < a.M * CPR) {
+          const int row = c / CPR, col = c - row * CPR;
+          *reinterpret_cast<float4_t*>(xs2 + row * XROW + col * 16) = tmp[u];
+        }
+      }
     }
     __syncthreads();
     CT_MARK(CT_VOCAB, 1 + h);  // this half of the rows staged
@@ -859,13 +886,22 @@ __global__ __launch_bounds__(1024) void k_vocab_2p(GemmArgs a) {
   // lane holds rows mt*16 + r, columns tile*16 + 4g .. +3
   const int n = tile * 16 + 4 * g;
   const auto rs = wt_rsrc(a.out_f32);
+  // (no bias: the launcher requires none; a conditional bias load here made the compiler
+  // wait vmcnt(0) before every store — 28 serialized write-through stores, ~30 of 61 us)
+  const float4_t(&ov)[MT] = acc;
+  const bool full = n + 3 < a.N;
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt) {
     const int m = mt * 16 + r;
     if (m < a.M) {
+      if (full) {
 #pragma unroll
-      for (int e = 0; e < 4; ++e)
-        if (n + e < a.N) wt_store1(rs, (m * a.ldo + n + e) * 4, acc[mt][e] + (a.bias ? a.bias[n + e] : 0.f));
+        for (int e = 0; e < 4; ++e) wt_store1(rs, (m * a.ldo + n + e) * 4, ov[mt][e]);
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          if (n + e < a.N) wt_store1(rs, (m * a.ldo + n + e) * 4, ov[mt][e]);
+      }
     }
   }
   CT_END(CT_VOCAB);
@@ -1110,7 +1146,7 @@ int launch_gemm_tiles(const GemmArgs& a, int epi, int tile_sel, hipStream_t st) 
     const int vgrp = (a.M + vrg_max - 1) / vrg_max;
     // (<= 32 rows: at 100 rows, 2 groups of 50, it measured 89.2 us against k_gemv_x's 84.6:
     // each CU streams its column block twice, profiles/r03/vocab_groups_ab.txt)
-    if (vocab_small && epi == EPI_F32_COLS && a.N >= 16384 && a.M <= (sizeof(T) == 2 ? 32 : 16) && vgrp <= 4 &&
+    if (vocab_small && epi == EPI_F32_COLS && !a.bias && a.N >= 16384 && a.M <= (sizeof(T) == 2 ? 32 : 16) && vgrp <= 4 &&
         a.K <= 1280 && a.K % 32 == 0) {
       const int rg = (a.M + vgrp - 1) / vgrp, mtv = (rg + 15) / 16;
       const int lds = rg * vxrow;
@@ -1133,7 +1169,8 @@ int launch_gemm_tiles(const GemmArgs& a, int epi, int tile_sel, hipStream_t st) 
       }
     }
     // k_vocab_2p: 33..112 fp16 rows resident in LDS, half of K per pass
-    if (sizeof(T) == 2 && vocab_small && epi == EPI_F32_COLS && a.N >= 16384 && a.M > 32 && a.M <= 112 && !a.xf32 &&
+    if (sizeof(T) == 2 && vocab_small && epi == EPI_F32_COLS && !a.bias && a.N >= 16384 && a.M > 32 && a.M <= 112 &&
+        !a.xf32 &&
         a.K == 1280 && a.M * (a.K + 16) <= 150 * 1024) {
       // two 4-step weight chunks in flight per wave (DEPTH 3; WHISPER_HIP_V2P_DEPTH=2 in the
       // tuning build: one 5-step chunk) — step graph 3.5456 -> 3.5413 ms at 20 windows,

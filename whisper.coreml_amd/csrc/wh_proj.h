@@ -20,6 +20,10 @@
 #ifndef WH_PROJ_KZ_SLOW
 #define WH_PROJ_KZ_SLOW 0
 #endif
+// WH_PROJ_XSLOW=1 (A/B build): the general X-slice addressing for every launch
+#ifndef WH_PROJ_XSLOW
+#define WH_PROJ_XSLOW 0
+#endif
 
 namespace wh {
 
@@ -60,26 +64,51 @@ __global__ __launch_bounds__(64 * NSUB * KW) void k_proj(GemmArgs a) {
 
   // 1. X slice -> registers
   const char* X = reinterpret_cast<const char*>(a.X);
-  // source row of each chunk (-1: padding row -> zeros); the optional gather is
-  // resolved for every chunk before the first X load so no wait sits between them
-  int xr[P::XC];
-#pragma unroll
-  for (int i = 0; i < P::XC; ++i) {
-    const int c = tid + NT * i, m = m0 + c / P::CPR;
-    xr[i] = (c < P::MR * P::CPR && m < a.M) ? m : -1;
-  }
-  if (a.x_rows) {
-#pragma unroll
-    for (int i = 0; i < P::XC; ++i)
-      if (xr[i] >= 0) xr[i] = a.x_rows[xr[i]];
-  }
   float4_t xv[P::XC];
+  if (!a.x_rows && !WH_PROJ_XSLOW) {
+    // (the decoder step: no gather) chunk c = tid + NT i sits at row c / CPR, column c % CPR;
+    // both advance by compile-time steps, so the addresses are a few adds per chunk on a
+    // 32-bit buffer offset (the general form below spent ~20 instructions and a branch per
+    // chunk, ~0.7 us before the first weight load left), and every load is issued
+    // unconditionally: rows past M read row M - 1 (their MFMA outputs are never stored)
+    constexpr int DR = NT / P::CPR, DC = NT % P::CPR;
+    const int ldx2 = a.ldx * (int)sizeof(T);
+    // the buffer covers this workgroup's valid rows only: chunks of rows >= M read 0 (the
+    // padding rows' zeros, as the general form), with no clamp or branch per chunk
+    const auto rsx = __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(X) + ((int64_t)m0 * a.ldx + kb) * (int)sizeof(T),
+                                                       0, (a.M - m0) * ldx2 - kb * (int)sizeof(T), 0x00020000);
+    int col = tid % P::CPR, off = (tid / P::CPR) * ldx2 + col * 16;
 #pragma unroll
-  for (int i = 0; i < P::XC; ++i) {
-    const int c = tid + NT * i, col = c % P::CPR;
-    xv[i] = (float4_t){0.f, 0.f, 0.f, 0.f};
-    if (xr[i] >= 0)
-      xv[i] = *reinterpret_cast<const float4_t*>(X + ((int64_t)xr[i] * a.ldx + kb) * (int)sizeof(T) + col * 16);
+    for (int i = 0; i < P::XC; ++i) {
+      xv[i] = __builtin_bit_cast(float4_t, __builtin_amdgcn_raw_buffer_load_b128(rsx, off, 0, 0));
+      col += DC;
+      off += DR * ldx2 + DC * 16;
+      if (col >= P::CPR) {
+        col -= P::CPR;
+        off += ldx2 - P::CPR * 16;
+      }
+    }
+  } else {
+    // source row of each chunk (-1: padding row -> zeros); the optional gather is
+    // resolved for every chunk before the first X load so no wait sits between them
+    int xr[P::XC];
+#pragma unroll
+    for (int i = 0; i < P::XC; ++i) {
+      const int c = tid + NT * i, m = m0 + c / P::CPR;
+      xr[i] = (c < P::MR * P::CPR && m < a.M) ? m : -1;
+    }
+    if (a.x_rows) {
+#pragma unroll
+      for (int i = 0; i < P::XC; ++i)
+        if (xr[i] >= 0) xr[i] = a.x_rows[xr[i]];
+    }
+#pragma unroll
+    for (int i = 0; i < P::XC; ++i) {
+      const int c = tid + NT * i, col = c % P::CPR;
+      xv[i] = (float4_t){0.f, 0.f, 0.f, 0.f};
+      if (xr[i] >= 0)
+        xv[i] = *reinterpret_cast<const float4_t*>(X + ((int64_t)xr[i] * a.ldx + kb) * (int)sizeof(T) + col * 16);
+    }
   }
   // 2. the wave's weight fragments
   const T* wp = reinterpret_cast<const T*>(a.W) + (int64_t)min(n0 + r, a.N - 1) * a.K + kb + kw * NSTEP * 32 + 8 * g;
