@@ -69,6 +69,10 @@ inline void wh_launched(const char* name) {
     wh_first_launch_error() = std::string("launch of ") + name + ": " + hipGetErrorString(e);
 #endif
 }
+// a launcher that refuses its operands records why (surfaces at the entry point's check)
+inline void wh_set_launch_error(const char* msg) {
+  if (wh_first_launch_error().empty()) wh_first_launch_error() = msg;
+}
 
 // Chain trace (tuning build only, profiles/chain_trace.py): per-workgroup wall-clock marks
 // (s_memrealtime, 100 MHz) of the decoder-step kernels, one slot per kernel role; every
@@ -120,6 +124,10 @@ static __device__ unsigned long long g_ct_trace[CT_SLOTS][CT_WG][4];
 // which leaves every fp16 probability (min subnormal 2^-24) and every fp32 sum that
 // includes the row maximum's 1 unchanged.
 WH_DEV float hw_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
+// floor(b * n / nb) of a contiguous range split (workgroup b of nb takes [split(b), split(b + 1))),
+// in 32-bit unsigned arithmetic: b * n < 2^32 at every call site (<= 256 workgroups x
+// < 2^24 units).  The int64 form is a ~140-instruction scalar divide ahead of the first load.
+WH_DEV int range_split(int b, int n, int nb) { return (int)(((unsigned)b * (unsigned)n) / (unsigned)nb); }
 typedef float f32x2_t __attribute__((ext_vector_type(2)));  // packed fp32 (v_pk_add_f32 / v_pk_mul_f32)
 
 WH_DEV_HOST int xv_perm(int t) {

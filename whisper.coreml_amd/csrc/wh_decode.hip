@@ -1169,7 +1169,7 @@ __global__ __launch_bounds__(512) void k_vocab_sel(GemmArgs a, VsArgs v) {
   VS_MARK(0);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = lane & 15, g = lane >> 4;
   const int nt = (a.N + 15) / 16, b = blockIdx.x, nb = gridDim.x;
-  const int t0 = (int)((int64_t)b * nt / nb), t1 = (int)((int64_t)(b + 1) * nt / nb), ntl = t1 - t0;
+  const int t0 = range_split(b, nt, nb), t1 = range_split(b + 1, nt, nb), ntl = t1 - t0;
   const half_t* W = reinterpret_cast<const half_t*>(a.W);
   const int kb = wave * SW * 32;
   // 1. the window's state first (its loads retire first), then the LayerNorm operands,
@@ -1394,8 +1394,8 @@ __global__ __launch_bounds__(512) void k_vocab_sel(GemmArgs a, VsArgs v) {
   // 7. the combine, one wave per row: text records of the workgroups with columns below
   // timestamp_begin (lane j: workgroups j, j + 64, ...), timestamp records of those above
   if (lnrow) {
-    auto col0 = [&](int wb) { return (int)((int64_t)wb * nt / nb) * 16; };
-    auto col1 = [&](int wb) { return min((int)((int64_t)(wb + 1) * nt / nb) * 16, a.N); };
+    auto col0 = [&](int wb) { return range_split(wb, nt, nb) * 16; };
+    auto col1 = [&](int wb) { return min(range_split(wb + 1, nt, nb) * 16, a.N); };
     const auto rsr = wt_rsrc(v.rec);
     auto ld = [&](int part, int wb, int word) -> float {
       return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(

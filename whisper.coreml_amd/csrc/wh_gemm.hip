@@ -701,7 +701,7 @@ __global__ __launch_bounds__(512) void k_vocab1(GemmArgs a) {
   float4_t* red = reinterpret_cast<float4_t*>(xs1 + 8 * XROW);  // [TMAX tiles][KW][64]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = lane & 15, g = lane >> 4;
   const int nt = (a.N + 15) / 16, b = blockIdx.x, nb = gridDim.x;
-  const int t0 = (int)((int64_t)b * nt / nb), t1 = (int)((int64_t)(b + 1) * nt / nb), ntl = t1 - t0;
+  const int t0 = range_split(b, nt, nb), t1 = range_split(b + 1, nt, nb), ntl = t1 - t0;
   const half_t* W = reinterpret_cast<const half_t*>(a.W);
   const int kb = wave * SW * 32;
   auto load_tile = [&](int tl, Frag<half_t> (&wf)[SW]) {
@@ -807,7 +807,7 @@ __global__ __launch_bounds__(1024) void k_vocab_2p(GemmArgs a) {
   constexpr int K = 2 * KH;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = lane & 15, g = lane >> 4;
   const int nt = (a.N + 15) / 16;
-  const int t0 = (int)((int64_t)blockIdx.x * nt / gridDim.x), t1 = (int)((int64_t)(blockIdx.x + 1) * nt / gridDim.x);
+  const int t0 = range_split(blockIdx.x, nt, gridDim.x), t1 = range_split(blockIdx.x + 1, nt, gridDim.x);
   const int tile = t0 + wave;
   const bool act = tile < t1;
   const half_t* X = reinterpret_cast<const half_t*>(a.X);

@@ -1204,10 +1204,12 @@ template <typename T, int ACT, typename S = float>
 __global__ __launch_bounds__(256) void k_reduce_store(const S* __restrict__ part, int nsplit, int64_t part_stride,
                                                       const float* __restrict__ bias, T* __restrict__ out, int ldo, int M,
                                                       int N) {
-  const int64_t i = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4;
+  // 32-bit index arithmetic (M x N < 2^31, launch_reduce_store): the int64 divide was
+  // ~150 vector instructions ahead of the first slab load
+  const int i = (int)(blockIdx.x * 256 + threadIdx.x) * 4;
   CT_MARK(CT_REDUCE, 0);
-  if (i >= (int64_t)M * N) return;
-  const int m = (int)(i / N), n = (int)(i - (int64_t)m * N);
+  if (i >= M * N) return;
+  const int m = (int)((unsigned)i / (unsigned)N), n = i - m * N;
   typedef typename std::conditional<sizeof(S) == 2, half4_t, float4_t>::type R4;  // raw slab elements
   R4 pp[16];
 #pragma unroll
@@ -1229,6 +1231,10 @@ template <typename T>
 void launch_reduce_store(const float* part, int nsplit, int64_t part_stride, const float* bias, T* out, int ldo, int M,
                          int N, int gelu, hipStream_t st, int slab_half) {
   if (M <= 0) return;
+  if ((int64_t)M * N >= (int64_t)1 << 31) {
+    wh_set_launch_error("launch_reduce_store: M x N >= 2^31");
+    return;
+  }
   const int64_t tot = (int64_t)M * N / 4;
   const unsigned nb = (unsigned)((tot + 255) / 256);
   if (slab_half) {
@@ -1510,24 +1516,28 @@ __global__ __launch_bounds__(512, 1) void k_xattn_seg(const T* __restrict__ q, i
   constexpr int NW = 8, SMAX = XsShape<RR>::SMAX, PPASS = 512 / (RR * 16);  // pairs merged per pass
   constexpr bool QP = QZ > 0;
   __shared__ float seg_m[SMAX][RR], seg_l[SMAX][RR];
-  __shared__ float seg_o[SMAX][64][RR + 1];
+  // partial outputs row-major, 68-float rows: a lane's 4 columns are one 16-B store / load
+  // (tile(): lanes r = 0..7 of a store group hit banks 4r.. +3, conflict-free; round 4 kept
+  // [tile][64][RR + 1] and moved them as 16 + 4 single floats)
+  __shared__ __attribute__((aligned(16))) float seg_o[SMAX][RR][68];
   __shared__ __attribute__((aligned(16))) T qs[XS_QP][16][72];
   __shared__ int s_ticket[2];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int r = lane & 15, g = lane >> 4;
   const int nseg = npair * nsp, nwg = gridDim.x, b = blockIdx.x;
-  const int s0 = (int)((int64_t)b * nseg / nwg), s1 = (int)((int64_t)(b + 1) * nseg / nwg), cnt = s1 - s0;
+  const int s0 = range_split(b, nseg, nwg), s1 = range_split(b + 1, nseg, nwg), cnt = s1 - s0;
   const int pa = s0 / nsp, plast = (s1 - 1) / nsp;
   XS_MARK(0);
   CT_MARK(CT_XATTN, 0);
 
   // local tile i: K and V fragments
-  auto load_kv = [&](int i, Frag<T>(&kf)[4][2], Frag<T>(&vf)[4][2]) {
+  // (wsl >= 0: the tile's window slot, already loaded)
+  auto load_kv = [&](int i, Frag<T>(&kf)[4][2], Frag<T>(&vf)[4][2], int wsl = -1) {
     // i is wave-uniform: the tile's window slot comes by a scalar load (lgkmcnt).  Round 4:
     // as a vector load it sat in vmcnt order, and the s_waitcnt vmcnt(0) before the K / V
     // addresses drained the tile in flight: one tile per wave in flight, not two
     const int gs = __builtin_amdgcn_readfirstlane(s0 + i), p = gs / nsp, k = gs - p * nsp, wi = p / H, h = p - wi * H;
-    const int64_t off = (int64_t)win_slot[wi] * win_stride;
+    const int64_t off = (int64_t)(wsl >= 0 ? wsl : win_slot[wi]) * win_stride;
     const T* kbase = ck + off + (int64_t)h * TKP * 64;
     const T* vbase = cvt + off + (int64_t)h * 64 * TKP;
     const int kt0 = k * 64;
@@ -1591,8 +1601,7 @@ __global__ __launch_bounds__(512, 1) void k_xattn_seg(const T* __restrict__ q, i
       }
 #pragma unroll
       for (int dt = 0; dt < 4; ++dt)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) seg_o[i][dt * 16 + 4 * g + j][r] = acc[dt][j];
+        *reinterpret_cast<float4_t*>(&seg_o[i][r][dt * 16 + 4 * g]) = acc[dt];
     }
   };
 
@@ -1611,12 +1620,23 @@ __global__ __launch_bounds__(512, 1) void k_xattn_seg(const T* __restrict__ q, i
     if (wave < cnt) load_kv(wave, kA, vA);
   }
   float4_t qld[NQP][QP ? QZ + 1 : 1];  // QP: the QZ slabs, then the bias
+  // wave-uniform pairs: their windows' metadata by scalar loads (lgkmcnt, not behind
+  // vmcnt), all issued before the first use: one round trip, not one per load and pass
+  int q_hj[NQP], q_nr[NQP], q_r0[NQP];
 #pragma unroll
   for (int pass = 0; pass < NQP; ++pass) {
-    const int j = 2 * pass + (tid >> 8), t = tid & 255;
-    // wave-uniform pair: its window's metadata by scalar loads (lgkmcnt, not behind vmcnt)
-    const int pj = __builtin_amdgcn_readfirstlane(min(pa + j, plast)), wj = pj / H, hj = pj - wj * H;
-    const int qq = min(t >> 4, win_nrows[wj] - 1), c = hj * 64 + (t & 15) * 4, row = win_row0[wj] + qq;
+    const int pj = __builtin_amdgcn_readfirstlane(min(pa + 2 * pass + (tid >> 8), plast)), wj = pj / H;
+    q_hj[pass] = pj - wj * H;
+    q_nr[pass] = win_nrows[wj];
+    q_r0[pass] = win_row0[wj];
+  }
+  // FULL: the first tile's window slot rides in the same round trip
+  const int slot0 = FULL ? win_slot[__builtin_amdgcn_readfirstlane(s0 + wave) / nsp / H] : -1;
+  __builtin_amdgcn_sched_barrier(0);  // (else the second pass's loads sink below the first's wait)
+#pragma unroll
+  for (int pass = 0; pass < NQP; ++pass) {
+    const int t = tid & 255;
+    const int qq = min(t >> 4, q_nr[pass] - 1), c = q_hj[pass] * 64 + (t & 15) * 4, row = q_r0[pass] + qq;
     if constexpr (QP) {
       const S* src = reinterpret_cast<const S*>(xq.part) + (int64_t)row * ldq + c;
 #pragma unroll
@@ -1649,7 +1669,7 @@ __global__ __launch_bounds__(512, 1) void k_xattn_seg(const T* __restrict__ q, i
   // FULL: unconditional (every wave has a tile), so no branch join: behind one the
   // compiler's vmcnt bookkeeping made the query staging wait for the K / V loads as well
   if constexpr (FULL) {
-    load_kv(wave, kA, vA);
+    load_kv(wave, kA, vA, slot0);
     __builtin_amdgcn_sched_barrier(0);
   }
   stage_q();
@@ -1694,13 +1714,12 @@ __global__ __launch_bounds__(512, 1) void k_xattn_seg(const T* __restrict__ q, i
         emit(pj, xs_merge(nsp, [&](int k, float& m, float& l, float4_t& o) {
                m = seg_m[l0 + k][qq];
                l = seg_l[l0 + k][qq];
-               o = (float4_t){seg_o[l0 + k][dc][qq], seg_o[l0 + k][dc + 1][qq], seg_o[l0 + k][dc + 2][qq],
-                              seg_o[l0 + k][dc + 3][qq]};
+               o = *reinterpret_cast<const float4_t*>(&seg_o[l0 + k][qq][dc]);
              }));
       } else {  // cut: this workgroup's partials of the pair -> records [pair][tile]
         for (int s = max(l0, 0); s < min(l1, cnt); ++s) {
           const int rb = (pj * nsp + (s - l0)) * XREC * 4;
-          const float4_t o = (float4_t){seg_o[s][dc][qq], seg_o[s][dc + 1][qq], seg_o[s][dc + 2][qq], seg_o[s][dc + 3][qq]};
+          const float4_t o = *reinterpret_cast<const float4_t*>(&seg_o[s][qq][dc]);
           __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, o), rs, rb + (qq * 64 + dc) * 4, 0, 16);
           if (dc == 0) {
             __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, seg_m[s][qq]), rs, rb + (1024 + qq) * 4, 0, 16);
