@@ -40,13 +40,14 @@ for u in UNITS:
     getattr(lib, f"wh_tune_ct_trace_{u}").restype = ctypes.c_int
     getattr(lib, f"wh_tune_ct_clear_{u}").restype = ctypes.c_int
 SLOT_UNIT = {0: "proj", 1: "proj", 2: "proj", 3: "proj", 4: "kernels", 5: "kernels", 6: "kernels", 7: "kernels",
-             8: "gemm", 9: "decode", 10: "decode"}
+             8: "gemm", 9: "decode", 10: "decode", 11: "decode"}
 ORDER = [(0, "qkv k_proj", ("X staged", "MFMA done")), (6, "self-attn (+qkv reduce)", None),
          (7, "cross-attn k_xattn_seg", None), (1, "cross-out k_proj", ("X staged", "MFMA done")),
          (2, "fc1 k_proj", ("X staged", "MFMA done")), (5, "reduce+GELU", None),
          (3, "fc2 k_proj", ("X staged", "MFMA done")), (4, "resid+LN (final)", ("loads landed", None)),
          (8, "vocab k_vocab_2p / k_vocab1", ("half 0 staged", "half 1 staged")), (9, "selection k_logit_part", ("row combine", "window merge")),
-         (10, "  merge_window (in it)", ("staged", "ranked"))]
+         (10, "  merge_window (in it)", ("staged", "ranked")),
+         (11, "  selection slices (marks)", ("loads", "top-k"))]
 
 m.ctx.decode_begin(task.wh_opts(), [task.initial_tokens] * W, [task.sot_index] * W)
 m.ctx.time_stage(0, 2 + ADVANCE)  # graph captured, warm; ADVANCE more tokens of context
@@ -58,7 +59,7 @@ for rep in range(REPS):
     steps.append(m.ctx.time_stage(0, 1))
     tr = {}
     for u in UNITS:
-        buf = np.zeros((11, 2048, 4), dtype=np.uint64)
+        buf = np.zeros((12, 2048, 4), dtype=np.uint64)
         assert getattr(lib, f"wh_tune_ct_trace_{u}")(buf.ctypes.data) == 0
         tr[u] = buf.astype(np.int64)
     base = None

@@ -80,9 +80,10 @@ inline void wh_set_launch_error(const char* msg) {
 // launch (layer 31's).  Mark 0 = workgroup start, 1 / 2 = kernel-specific phase ends,
 // 3 = thread 0 done (its stores drained).  Each translation unit has its own copy of the
 // array (static) and reader (WH_CT_READER); the slots of one role live in one unit.
-constexpr int CT_SLOTS = 11, CT_WG = 2048;
+constexpr int CT_SLOTS = 12, CT_WG = 2048;
 enum { CT_PROJ_QKV = 0, CT_PROJ_NN = 1, CT_PROJ_FC1 = 2, CT_PROJ_FC2 = 3, CT_RESID_LN = 4, CT_REDUCE = 5,
-       CT_SELF_ATTN = 6, CT_XATTN = 7, CT_VOCAB = 8, CT_LOGIT = 9, CT_MERGE = 10 };
+       CT_SELF_ATTN = 6, CT_XATTN = 7, CT_VOCAB = 8, CT_LOGIT = 9, CT_MERGE = 10,
+       CT_LOGIT_SLICE = 11 };  // k_logit_part slice phases: 0 loads landed, 1 top-k, 2 record stored, 3 arrived
 #if WH_TUNING
 static __device__ unsigned long long g_ct_trace[CT_SLOTS][CT_WG][4];
 #define CT_MARK(slot, k)                                                                 \
@@ -124,6 +125,10 @@ static __device__ unsigned long long g_ct_trace[CT_SLOTS][CT_WG][4];
 // which leaves every fp16 probability (min subnormal 2^-24) and every fp32 sum that
 // includes the row maximum's 1 unchanged.
 WH_DEV float hw_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
+// workgroup barrier for LDS data only: waits for this wave's LDS operations, not for its
+// global loads / stores in flight (__syncthreads waits vmcnt(0) too: a store round trip of
+// ~1-2 us when the wave has just written global memory nobody in the workgroup reads)
+WH_DEV void wh_lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 // floor(b * n / nb) of a contiguous range split (workgroup b of nb takes [split(b), split(b + 1))),
 // in 32-bit unsigned arithmetic: b * n < 2^32 at every call site (<= 256 workgroups x
 // < 2^24 units).  The int64 form is a ~140-instruction scalar divide ahead of the first load.

@@ -366,7 +366,7 @@ __device__ __forceinline__ void merge_window(const DecState& s, const DecOpts& o
     if (em.x) {
       const int pos = min(len - 1, em.pmax);
       if (tid < G) L.etok[tid] = hist[tid * s.hctx + pos];
-      __syncthreads();
+      wh_lds_barrier();
       merge_embed<NT>(em, w, G, pos, L.etok, tid);
     }
     CT_END(CT_MERGE);
@@ -391,7 +391,7 @@ __device__ __forceinline__ void merge_window(const DecState& s, const DecOpts& o
       hist[tid * s.hctx + len] = t;
       L.tok[tid] = t;
     }
-    __syncthreads();
+    wh_lds_barrier();
     if (tid == 0) {
       int all_eot = 1;
       for (int b = 0; b < G; ++b) all_eot &= (L.tok[b] == o.eot);
@@ -403,7 +403,7 @@ __device__ __forceinline__ void merge_window(const DecState& s, const DecOpts& o
     if (em.x) {
       const int pos = min(len, em.pmax);  // the new length is len + 1
       if (tid < G) L.etok[tid] = pos == len ? L.tok[tid] : hist[tid * s.hctx + pos];  // pos < len: not written here
-      __syncthreads();
+      wh_lds_barrier();
       merge_embed<NT>(em, w, G, pos, L.etok, tid);
     }
     CT_END(CT_MERGE);
@@ -450,7 +450,7 @@ __device__ __forceinline__ void merge_window(const DecState& s, const DecOpts& o
     L.ctok[tid] = ct;
     L.csrc[tid] = first ? (G - 1) : tid / (G + 1);
   }
-  __syncthreads();
+  wh_lds_barrier();
   CT_MARK(CT_MERGE, 1);  // histories, ancestry and candidates staged
   // stable descending sort by rank (ties keep insertion order), then the walk of
   // decoding.py:375-386 in closed form: the candidate at rank q is taken iff fewer
@@ -502,7 +502,7 @@ __device__ __forceinline__ void merge_window(const DecState& s, const DecOpts& o
       for (int c = 0; c < nc; ++c) q += (L.csc[c] > sc) || (L.csc[c] == sc && c < c0);
       L.rk[c0] = q;
     }
-    __syncthreads();
+    wh_lds_barrier();
     for (int c0 = tid; c0 < nc; c0 += NT) {
       const int q = L.rk[c0];
       int ne = 0, ee = 0;  // non-EOT / EOT candidates ranked above
@@ -514,7 +514,7 @@ __device__ __forceinline__ void merge_window(const DecState& s, const DecOpts& o
       take(c0, ne, ee, L.csc[c0], L.ctok[c0], L.csrc[c0]);
     }
   }
-  __syncthreads();
+  wh_lds_barrier();
   CT_MARK(CT_MERGE, 2);  // ranked and walked
   // new histories / ancestry
   for (int i = tid; i < G * (len + 1); i += NT) {
@@ -533,7 +533,7 @@ __device__ __forceinline__ void merge_window(const DecState& s, const DecOpts& o
     s.fin_score[w * s.maxc + fin0 + tid] = L.fsc[tid];
     s.fin_len[w * s.maxc + fin0 + tid] = len + 1;
   }
-  __syncthreads();
+  wh_lds_barrier();
   if (tid == 0) {
     const int fn = fin0 + nadd;
     s.fin_n[w] = fn;
@@ -546,7 +546,7 @@ __device__ __forceinline__ void merge_window(const DecState& s, const DecOpts& o
     // row j's new history is oh[src[j]][0, len) + tok[j]: its input token from LDS
     const int pos = min(len, em.pmax);
     if (tid < G) L.etok[tid] = pos == len ? L.tok[tid] : L.oh[L.src[tid]][pos];
-    __syncthreads();
+    wh_lds_barrier();
     merge_embed<NT>(em, w, G, pos, L.etok, tid);
   }
   CT_END(CT_MERGE);
@@ -662,6 +662,10 @@ __global__ __launch_bounds__(LP_THREADS) WH_LP_ATTR void k_logit_part(float* __r
     xv[u] = row[ic];
     sw[u] = o.suppress ? o.suppress[ic >> 5] : 0u;
   }
+  // the whole history row, one position per thread (hctx <= LP_THREADS, the launcher), in
+  // the same round trip: its addresses do not wait for the window's len / sample_begin
+  const int* hist = s.hist + (int64_t)r * s.hctx;
+  const int hp = hist[min(tid, s.hctx - 1)];
   const int done = s.done[w], len = s.len[w], sb = s.sample_begin[w];
   if (done) {
     if constexpr (MERGE)
@@ -669,19 +673,20 @@ __global__ __launch_bounds__(LP_THREADS) WH_LP_ATTR void k_logit_part(float* __r
     return;
   }
   // 2. history facts (decoding.py:503-508): the last timestamp token of the sampled
-  // part (len - sb <= 448 < LP_THREADS: one position per thread) and the last two tokens
-  const int* hist = s.hist + (int64_t)r * s.hctx;
-  const int p = sb + tid;
-  const int hp = hist[min(p, max(len - 1, 0))];
-  const int h1 = hist[max(len - 1, 0)], h2 = hist[max(len - 2, 0)];
-  int pm = (p < len && hp >= tb) ? p : -1, pt = hp;
+  // part [sb, len) and the last two tokens (through LDS, across the barrier)
+  __shared__ int s_h12[2];
+  if (tid == max(len - 1, 0)) s_h12[0] = hp;
+  if (tid == max(len - 2, 0)) s_h12[1] = hp;
+  int pm = (tid >= sb && tid < len && hp >= tb) ? tid : -1, pt = hp;
 #pragma unroll
   for (int o2 = 32; o2 > 0; o2 >>= 1) {
     const int op = __shfl_xor(pm, o2, 64), ot = __shfl_xor(pt, o2, 64);
     if (op > pm) { pm = op; pt = ot; }
   }
   if (lane == 0) { pm_w[wv] = pm; pt_w[wv] = pt; }
-  __syncthreads();
+  wh_lds_barrier();
+  CT_MARK(CT_LOGIT_SLICE, 0);
+  const int h1 = s_h12[0], h2 = s_h12[1];
   int PM = -1, PT = -1;
 #pragma unroll
   for (int k = 0; k < NWV; ++k)
@@ -748,10 +753,12 @@ __global__ __launch_bounds__(LP_THREADS) WH_LP_ATTR void k_logit_part(float* __r
   __shared__ __attribute__((aligned(16))) float recs[FUSED ? NS * LP_REC : 4];
   // (wave 0) returns true when this combine completed the window (MERGE)
   auto arrive_and_combine = [&]() -> bool {
+    CT_MARK(CT_LOGIT_SLICE, 2);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     int ticket = 0;
     if (lane == 0) ticket = __hip_atomic_fetch_add(s.lp_cnt + r, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     ticket = __shfl(ticket, 0, 64);
+    CT_MARK(CT_LOGIT_SLICE, 3);
     if (ticket != NS - 1) return false;
     CT_MARK(CT_LOGIT, 1);  // this workgroup combines its row
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // no instruction: keeps the loads below the add
@@ -781,7 +788,7 @@ __global__ __launch_bounds__(LP_THREADS) WH_LP_ATTR void k_logit_part(float* __r
   auto finish = [&](bool go) {
     if constexpr (MERGE) {
       if (wv == 0 && lane == 0) s_go = go;
-      __syncthreads();
+      wh_lds_barrier();
       if (s_go) {
         CT_MARK(CT_LOGIT, 2);  // this workgroup merges its window
         merge_window<LP_THREADS, true>(s, o, em, w, tid, mlds);
@@ -833,7 +840,8 @@ __global__ __launch_bounds__(LP_THREADS) WH_LP_ATTR void k_logit_part(float* __r
       if (lane == 0) { wv_v[wv][q] = bv; wv_i[wv][q] = bi; }
     }
   }
-  __syncthreads();
+  wh_lds_barrier();
+  CT_MARK(CT_LOGIT_SLICE, 1);
   if (!MERGE && wv != 0) return;
   bool go = false;
   if (wv == 0) {
@@ -1013,6 +1021,7 @@ static bool select_rows(float* logits, int ldl, const DecState& s, const DecOpts
   }();
   const int rows = nwin * s.G;
   const bool merge = em && fold_merge && s.lpw_cnt && s.G <= MG_MAXG;
+  const bool sp = split && s.hctx <= LP_THREADS;  // k_logit_part: one history position per thread
   const MergeEmbed none;
   const MergeEmbed& e = em ? *em : none;
   // the records merged by the row's last slice (fused) unless WHISPER_HIP_LP_FUSED=0 (tuning:
@@ -1030,13 +1039,13 @@ static bool select_rows(float* logits, int ldl, const DecState& s, const DecOpts
   const char* nse = tune_env("WHISPER_HIP_LP_NS");
   const int ns_force = nse ? atoi(nse) : 16;  // slices for >= 2 windows
   const bool one_win = nwin == 1;
-  if (split && fused && !one_win && ns_force == 16 && o.ts_begin > 0 &&
+  if (sp && fused && !one_win && ns_force == 16 && o.ts_begin > 0 &&
       (o.ts_begin + 14) / 15 <= LP_THREADS * 8 && o.V - o.ts_begin <= LP_THREADS * 8) {
     if (merge) k_logit_part<16, 8, true, true><<<dim3(rows, 16), LP_THREADS, 0, st>>>(logits, ldl, s, o, e), wh_launched("k_logit_part");
     else k_logit_part<16, 8, true><<<dim3(rows, 16), LP_THREADS, 0, st>>>(logits, ldl, s, o, e), wh_launched("k_logit_part");
     return merge;
   }
-  if (split && o.ts_begin > 0 && (one_win || ns_force == 32) && (o.ts_begin + 30) / 31 <= LP_THREADS * 4 &&
+  if (sp && o.ts_begin > 0 && (one_win || ns_force == 32) && (o.ts_begin + 30) / 31 <= LP_THREADS * 4 &&
       o.V - o.ts_begin <= LP_THREADS * 4) {
     if (fused) {
       if (merge) k_logit_part<32, 4, true, true><<<dim3(rows, 32), LP_THREADS, 0, st>>>(logits, ldl, s, o, e), wh_launched("k_logit_part");
@@ -1047,7 +1056,7 @@ static bool select_rows(float* logits, int ldl, const DecState& s, const DecOpts
     k_logit_combine<32><<<rows, 64, 0, st>>>(s, o), wh_launched("k_logit_combine");
     return false;
   }
-  if (split && o.ts_begin > 0 && (o.ts_begin + 6) / 7 <= LP_THREADS * 16 && o.V - o.ts_begin <= LP_THREADS * 16) {
+  if (sp && o.ts_begin > 0 && (o.ts_begin + 6) / 7 <= LP_THREADS * 16 && o.V - o.ts_begin <= LP_THREADS * 16) {
     if (fused) {
       if (merge) k_logit_part<8, 16, true, true><<<dim3(rows, 8), LP_THREADS, 0, st>>>(logits, ldl, s, o, e), wh_launched("k_logit_part");
       else k_logit_part<8, 16, true><<<dim3(rows, 8), LP_THREADS, 0, st>>>(logits, ldl, s, o, e), wh_launched("k_logit_part");
