@@ -205,8 +205,11 @@ int wh_token_ms(wh_ctx* ctx, float* out, int cap, int* n, int reset);
          4 = the token-selection kernel (k_logit_rows) on the current logits,
          5 / 6 = 2 / 3 on layer 0 only, repeated (operands Infinity-Cache warm),
          7 = the step's k_proj launches inside `iters` eager decoder steps, each timed by
-             its own dispatch events (advances the decode state like a step).
-   For 2, 3, 5, 6 and 7 *ms_per_iter is the average duration of a single kernel launch. */
+             its own dispatch events (advances the decode state like a step),
+         8 / 9 = the batched step's self-attention (k_self_attn_qkv) of every layer at the
+             current context, with the decode's ancestry (8) or every row reading beam slot
+             0's history (9: all beams share one history); the ancestry is restored.
+   For 2, 3, 5, 6, 7, 8 and 9 *ms_per_iter is the average duration of a single kernel launch. */
 int wh_time_stage(wh_ctx* ctx, int what, int iters, double* ms_per_iter);
 
 /* ---- audio file decoding (host only, no context / GPU needed) ----

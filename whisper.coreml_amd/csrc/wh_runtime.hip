@@ -871,6 +871,7 @@ struct Ctx : public wh_ctx {
   // in its prologue.
   // anc: the ancestry table the self-attention reads ([w][ancG][CTX]); the decode's S.anc
   // unless a first pass (alignment / prefill logits) gives its own (fp_anc: all zeros)
+  int sa_probe_ks = 1;  // the QKV projection's split count (time_stage 8 / 9)
   int dec_layers(int R, const int* rw, const int* rs, const int* rp, int ancG, int nwin, const int* wr0, const int* wnr,
                  const int* wsl, float* aqk, const int* qkmap, int qkrows, bool step = false,
                  const int* anc = nullptr) {
@@ -889,6 +890,7 @@ struct Ctx : public wh_ctx {
       if (skinny) {
         int ks = 0;
         TRY(partial(xn_d, n, e.wqkv, R, 3 * n, n, &ks, false));  // k_self_attn_qkv reads fp32 slabs
+        sa_probe_ks = ks;
         if (launch_self_attn_qkv<T>(part, ks, (int64_t)R * 3 * n, e.bqkv, n, kc[l], vc[l], rw, rs, rp, A, ancG,
                                     Gcap, nh, CTX, att_d, n, R, st, slab_h))
           return fail(-20, "self-attention rows are not a whole number of beam groups");
@@ -1795,6 +1797,42 @@ struct Ctx : public wh_ctx {
       proj_ev_n = 0;
       if (rc) return rc;
       *ms = launches ? tot / launches : 0.0;
+      return 0;
+    } else if (what == 8 || what == 9) {
+      // the step's self-attention alone (k_self_attn_qkv, every layer, the live batch at its
+      // current context; it rewrites each row's K/V at its next position from the slabs as
+      // they stand, which the next real step overwrites): 8 = the decode's ancestry, 9 = every
+      // row reading beam slot 0's rows (all beams share one history: the bytes an L2 that
+      // deduplicated shared rows perfectly would fetch).  Per-launch ms.
+      if (cur_nwin < 1 || cur_G < 1) return fail(-16, "no decode batch");
+      if (p1_active(cur_nwin * cur_G, cur_nwin)) return fail(-2, "time_stage(8/9): the single-window step has no k_self_attn_qkv");
+      const int R = cur_nwin * cur_G, n = ns;
+      const size_t ab = (size_t)Wcap * Gcap * CTX * sizeof(int);
+      int* saved = nullptr;
+      if (what == 9) {
+        HIPCHK(hipMalloc((void**)&saved, ab));
+        HIPCHK(hipMemcpyAsync(saved, S.anc, ab, hipMemcpyDeviceToDevice, st));
+        HIPCHK(hipMemsetAsync(S.anc, 0, ab, st));
+      }
+      int rc = 0;
+      if (hipEventRecord(tm.a, st) != hipSuccess) rc = fail(-100, "time_stage(8/9): hipEventRecord failed");
+      for (int i = 0; rc == 0 && i < iters; ++i)
+        for (int l = 0; rc == 0 && l < Ld; ++l)
+          if (launch_self_attn_qkv<T>(part, sa_probe_ks, (int64_t)R * 3 * n, dec[l].bqkv, n, kc[l], vc[l], st_row_win,
+                                      st_row_slot, row_pos, S.anc, cur_G, Gcap, nh, CTX, att_d, n, R, st, 0))
+            rc = fail(-20, "time_stage(8/9): self-attention launch refused");
+      if (rc == 0 && hipEventRecord(tm.b, st) != hipSuccess) rc = fail(-100, "time_stage(8/9): hipEventRecord failed");
+      if (saved) {
+        if (hipMemcpyAsync(S.anc, saved, ab, hipMemcpyDeviceToDevice, st) != hipSuccess && rc == 0)
+          rc = fail(-100, "time_stage(9): ancestry restore failed");
+        if (hipStreamSynchronize(st) != hipSuccess && rc == 0) rc = fail(-100, "time_stage(9): sync failed");
+        if (hipFree(saved) != hipSuccess && rc == 0) rc = fail(-100, "time_stage(9): hipFree failed");
+      }
+      if (rc) return rc;
+      HIPCHK(hipStreamSynchronize(st));
+      float t = 0;
+      HIPCHK(hipEventElapsedTime(&t, tm.a, tm.b));
+      *ms = t / (iters * Ld);
       return 0;
     } else if (what == 4) {
       // the token-selection kernel alone on the current logits (state unchanged)
