@@ -176,6 +176,19 @@ WH_DEV void frag_load_stream(Frag<float>& f, const float* p) {
 #endif
 }
 
+// 8 consecutive elements at byte offset `off` (< 2^31) of a buffer resource (wt_rsrc):
+// 32-bit address arithmetic instead of a 64-bit multiply chain per load
+template <typename R>
+WH_DEV void frag_load_buf(Frag<half_t>& f, R rs, int off) {
+  f.v = __builtin_bit_cast(half8_t, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0));
+}
+template <typename R>
+WH_DEV void frag_load_buf(Frag<float>& f, R rs, int off) {
+  const float4_t a = __builtin_bit_cast(float4_t, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0));
+  const float4_t b = __builtin_bit_cast(float4_t, __builtin_amdgcn_raw_buffer_load_b128(rs, off + 16, 0, 0));
+  f.v = (float8_t){a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+}
+
 // two groups of 4 consecutive elements (8 B each for half, 16 B for float)
 WH_DEV void load4x2(Frag<half_t>& f, const half_t* p0, const half_t* p1) {
   const half4_t a = *reinterpret_cast<const half4_t*>(p0), b = *reinterpret_cast<const half4_t*>(p1);

@@ -388,6 +388,13 @@ __global__ __launch_bounds__(64) void k_self_attn(const T* __restrict__ q, int l
   const int64_t head_stride = (int64_t)ctx * 64;
   const int64_t wbase = (int64_t)w * nbeam;
   auto kv_off = [&](int slot, int p) -> int64_t { return ((wbase + slot) * H + h) * head_stride + (int64_t)p * 64; };
+  // cached K / V reads: 32-bit byte offsets into buffer resources (a context caps one
+  // layer's cache below 2 GiB, wh_runtime.hip); slot_of holds each position's slot already
+  // multiplied by the slot stride, so an address is two adds and a shift (the int64 form
+  // was a chain of 64-bit multiplies per load: ~1 us of VALU per pass at 100 rows)
+  constexpr int TB = (int)sizeof(T), ROWB = 64 * TB;
+  const int slotB = H * ctx * ROWB, baseB = ((int)wbase * H + h) * ctx * ROWB;
+  const auto rk = wt_rsrc(kc), rv = wt_rsrc(vc);
   if constexpr (sizeof(T) == 2 && PIPE) {
     int sv[8];
 #pragma unroll
@@ -395,7 +402,7 @@ __global__ __launch_bounds__(64) void k_self_attn(const T* __restrict__ q, int l
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       const int pp = lane + 64 * i;
-      if (pp <= pos) slot_of[pp] = pp == pos ? sl : sv[i];
+      if (pp <= pos) slot_of[pp] = (pp == pos ? sl : sv[i]) * slotB;
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // one wave: its own LDS writes
     const int kg = lane >> 3, dc = (lane & 7) * 8;
@@ -404,13 +411,13 @@ __global__ __launch_bounds__(64) void k_self_attn(const T* __restrict__ q, int l
     for (int e = 0; e < 8; ++e) o[e] = 0.f;
     auto load = [&](int p0, Frag<T>(&k)[8], Frag<T>(&v)[8]) {
       const int pa = min(p0 + lane, pos);
-      const T* ra = kc + kv_off(slot_of[pa], pa);
+      const int ra = baseB + slot_of[pa] + pa * ROWB;
 #pragma unroll
-      for (int c = 0; c < 8; ++c) frag_load(k[c], ra + 8 * c);
+      for (int c = 0; c < 8; ++c) frag_load_buf(k[c], rk, ra + 8 * c * TB);
 #pragma unroll
       for (int u = 0; u < 8; ++u) {
         const int pc = min(p0 + kg + 8 * u, pos);
-        frag_load(v[u], vc + kv_off(slot_of[pc], pc) + dc);
+        frag_load_buf(v[u], rv, baseB + slot_of[pc] + pc * ROWB + dc * TB);
       }
     };
     auto pass = [&](int p0, const Frag<T>(&k)[8], const Frag<T>(&v)[8]) {
@@ -474,7 +481,7 @@ __global__ __launch_bounds__(64) void k_self_attn(const T* __restrict__ q, int l
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       const int pp = lane + 64 * i;
-      if (pp <= pos) slot_of[pp] = pp == pos ? sl : sv[i];
+      if (pp <= pos) slot_of[pp] = (pp == pos ? sl : sv[i]) * slotB;
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // one wave: its own LDS writes
     const int kg = lane >> 3, dc = (lane & 7) * 8;
@@ -483,17 +490,16 @@ __global__ __launch_bounds__(64) void k_self_attn(const T* __restrict__ q, int l
     for (int e = 0; e < 8; ++e) o[e] = 0.f;
     for (int p0 = 0; p0 <= pos; p0 += 128) {
       const int pa = min(p0 + lane, pos), pb = min(p0 + 64 + lane, pos);
-      const T* ra = kc + kv_off(slot_of[pa], pa);
-      const T* rb = kc + kv_off(slot_of[pb], pb);
+      const int ra = baseB + slot_of[pa] + pa * ROWB, rb = baseB + slot_of[pb] + pb * ROWB;
       Frag<T> ka[8], kb[8], vf[16];
 #pragma unroll
-      for (int c = 0; c < 8; ++c) frag_load(ka[c], ra + 8 * c);
+      for (int c = 0; c < 8; ++c) frag_load_buf(ka[c], rk, ra + 8 * c * TB);
 #pragma unroll
-      for (int c = 0; c < 8; ++c) frag_load(kb[c], rb + 8 * c);
+      for (int c = 0; c < 8; ++c) frag_load_buf(kb[c], rk, rb + 8 * c * TB);
 #pragma unroll
       for (int u = 0; u < 16; ++u) {
         const int pc = min(p0 + kg + 8 * u, pos);
-        frag_load(vf[u], vc + kv_off(slot_of[pc], pc) + dc);
+        frag_load_buf(vf[u], rv, baseB + slot_of[pc] + pc * ROWB + dc * TB);
       }
       __builtin_amdgcn_sched_barrier(0);  // every load of the pass ahead of the math
       float sa = 0.f, sb = 0.f;
@@ -540,14 +546,14 @@ __global__ __launch_bounds__(64) void k_self_attn(const T* __restrict__ q, int l
   // scores: lane per key
   float mx = -INFINITY;
   for (int p = lane; p <= pos; p += 64) {
-    const int slot = (p == pos) ? sl : an[p];
+    const int slot = ((p == pos) ? sl : an[p]) * slotB;
     slot_of[p] = slot;
-    const T* kr = kc + kv_off(slot, p);
+    const int kr = baseB + slot + p * ROWB;
     float s = 0.f;
 #pragma unroll
     for (int c = 0; c < 64; c += 8) {
       Frag<T> f;
-      frag_load(f, kr + c);
+      frag_load_buf(f, rk, kr + c * TB);
 #pragma unroll
       for (int e = 0; e < 8; ++e) s += qv[c + e] * to_f32(f.v[e]);
     }
@@ -572,7 +578,7 @@ __global__ __launch_bounds__(64) void k_self_attn(const T* __restrict__ q, int l
   for (; p + 24 <= pos; p += 32) {  // 4 keys per lane in flight
     Frag<T> f[4];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) frag_load(f[u], vc + kv_off(slot_of[p + 8 * u], p + 8 * u) + dc);
+    for (int u = 0; u < 4; ++u) frag_load_buf(f[u], rv, baseB + slot_of[p + 8 * u] + (p + 8 * u) * ROWB + dc * TB);
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const float pw = sc[p + 8 * u];
@@ -582,7 +588,7 @@ __global__ __launch_bounds__(64) void k_self_attn(const T* __restrict__ q, int l
   }
   for (; p <= pos; p += 8) {
     Frag<T> f;
-    frag_load(f, vc + kv_off(slot_of[p], p) + dc);
+    frag_load_buf(f, rv, baseB + slot_of[p] + p * ROWB + dc * TB);
     const float pw = sc[p];
 #pragma unroll
     for (int e = 0; e < 8; ++e) o[e] += pw * to_f32(f.v[e]);
@@ -656,6 +662,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void
   const int64_t head_stride = (int64_t)ctx * 64;
   const int64_t wbase = (int64_t)w * nbeam;
   auto kv_off = [&](int slot, int p) -> int64_t { return ((wbase + slot) * H + h) * head_stride + (int64_t)p * 64; };
+  // cached K / V reads: 32-bit byte offsets into buffer resources (a context caps one
+  // layer's cache below 2 GiB, wh_runtime.hip); slot_of holds each position's slot already
+  // multiplied by the slot stride, so an address is two adds and a shift (the int64 form
+  // was a chain of 64-bit multiplies per load: ~1 us of VALU per pass at 100 rows)
+  constexpr int TB = (int)sizeof(T), ROWB = 64 * TB;
+  const int slotB = H * ctx * ROWB, baseB = ((int)wbase * H + h) * ctx * ROWB;
+  const auto rk = wt_rsrc(kc), rv = wt_rsrc(vc);
   // one round trip for everything that does not depend on this step's projection:
   // the position, the ancestry slot of every context position (8 per lane, clamped to
   // the context, issued together) and the q/k/v partial slabs of this row and head
@@ -687,7 +700,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void
       }
   }
   for (int i = 0; i < 8; ++i)
-    if (lane + 64 * i < pos) slot_of[lane + 64 * i] = sv[i];
+    if (lane + 64 * i < pos) slot_of[lane + 64 * i] = sv[i] * slotB;
   const int plast = max(pos - 1, 0);
   const T qT = from_f32<T>(qd), kT = from_f32<T>(kd), vT = from_f32<T>(vd);
   kc[kv_off(sl, pos) + lane] = kT;
@@ -705,13 +718,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void
     for (int e = 0; e < 8; ++e) o[e] = 0.f;
     auto load = [&](int p0, Frag<T>(&k)[8], Frag<T>(&v)[8]) {
       const int pa = min(p0 + lane, plast);
-      const T* ra = kc + kv_off(slot_of[pa], pa);
+      const int ra = baseB + slot_of[pa] + pa * ROWB;
 #pragma unroll
-      for (int c = 0; c < 8; ++c) frag_load(k[c], ra + 8 * c);
+      for (int c = 0; c < 8; ++c) frag_load_buf(k[c], rk, ra + 8 * c * TB);
 #pragma unroll
       for (int u = 0; u < 8; ++u) {
         const int pc = min(p0 + kg + 8 * u, plast);
-        frag_load(v[u], vc + kv_off(slot_of[pc], pc) + dc);
+        frag_load_buf(v[u], rv, baseB + slot_of[pc] + pc * ROWB + dc * TB);
       }
     };
     auto pass = [&](int p0, const Frag<T>(&k)[8], const Frag<T>(&v)[8]) {
@@ -798,17 +811,16 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void
     for (int e = 0; e < 8; ++e) o[e] = 0.f;
     for (int p0 = 0; p0 < pos; p0 += 128) {
       const int pa = min(p0 + lane, plast), pb = min(p0 + 64 + lane, plast);
-      const T* ra = kc + kv_off(slot_of[pa], pa);
-      const T* rb = kc + kv_off(slot_of[pb], pb);
+      const int ra = baseB + slot_of[pa] + pa * ROWB, rb = baseB + slot_of[pb] + pb * ROWB;
       Frag<T> ka[8], kb[8], vf[16];
 #pragma unroll
-      for (int c = 0; c < 8; ++c) frag_load(ka[c], ra + 8 * c);
+      for (int c = 0; c < 8; ++c) frag_load_buf(ka[c], rk, ra + 8 * c * TB);
 #pragma unroll
-      for (int c = 0; c < 8; ++c) frag_load(kb[c], rb + 8 * c);
+      for (int c = 0; c < 8; ++c) frag_load_buf(kb[c], rk, rb + 8 * c * TB);
 #pragma unroll
       for (int u = 0; u < 16; ++u) {
         const int pc = min(p0 + kg + 8 * u, plast);
-        frag_load(vf[u], vc + kv_off(slot_of[pc], pc) + dc);
+        frag_load_buf(vf[u], rv, baseB + slot_of[pc] + pc * ROWB + dc * TB);
       }
       __builtin_amdgcn_sched_barrier(0);  // every load of the pass ahead of the math
       float sa = 0.f, sb = 0.f;
@@ -860,13 +872,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void
   float mx = s_cur;
   for (int p0 = 0; p0 < pos; p0 += 128) {
     const int pa = min(p0 + lane, plast), pb = min(p0 + 64 + lane, plast);
-    const T* ra = kc + kv_off(slot_of[pa], pa);
-    const T* rb = kc + kv_off(slot_of[pb], pb);
+    const int ra = baseB + slot_of[pa] + pa * ROWB, rb = baseB + slot_of[pb] + pb * ROWB;
     Frag<T> ka[8], kb[8];
 #pragma unroll
-    for (int c = 0; c < 8; ++c) frag_load(ka[c], ra + 8 * c);
+    for (int c = 0; c < 8; ++c) frag_load_buf(ka[c], rk, ra + 8 * c * TB);
 #pragma unroll
-    for (int c = 0; c < 8; ++c) frag_load(kb[c], rb + 8 * c);
+    for (int c = 0; c < 8; ++c) frag_load_buf(kb[c], rk, rb + 8 * c * TB);
     __builtin_amdgcn_sched_barrier(0);  // keep all 16 loads ahead of the math
     float sa = 0.f, sb = 0.f;
 #pragma unroll
@@ -907,7 +918,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
       const int pc = min(p0 + 8 * u, plast);
-      frag_load(f[u], vc + kv_off(slot_of[pc], pc) + dc);
+      frag_load_buf(f[u], rv, baseB + slot_of[pc] + pc * ROWB + dc * TB);
       pw[u] = p0 + 8 * u < pos ? sc[pc] : 0.f;
     }
     __builtin_amdgcn_sched_barrier(0);

@@ -372,6 +372,10 @@ struct Ctx : public wh_ctx {
     addA(((size_t)WE * nh * 64 * TKP + 64) * sizeof(T));  // encoder V^T (padding keys stay zero)
     addA((size_t)Wcap * 1500 * n * sizeof(T));
     addA((size_t)2 * Ld * Wcap * TKP * n * sizeof(T) + 65536);  // + slack: last key tile reads past TKP
+    // the self-attention kernels address one layer's self-K / V cache with 32-bit byte
+    // offsets (buffer loads, wh_kernels.hip k_self_attn / k_self_attn_qkv)
+    if ((int64_t)Wcap * Gcap * CTX * n * (int64_t)sizeof(T) >= ((int64_t)1 << 31) - 4096)
+      return fail(-3, "self-KV cache of one layer exceeds 2 GiB: lower max_windows or max_group");
     for (int l = 0; l < Ld; ++l) { addA((size_t)Wcap * Gcap * CTX * n * sizeof(T)); addA((size_t)Wcap * Gcap * CTX * n * sizeof(T)); }
     addA((size_t)RD * n * 4); addA((size_t)RD * n * sizeof(T)); addA((size_t)RD * n * sizeof(T)); addA((size_t)RD * n * sizeof(T));
     addA((size_t)RD * 4 * n * sizeof(T));
