@@ -1533,6 +1533,7 @@ __global__ __launch_bounds__(512, 1) void k_xattn_seg(const T* __restrict__ q, i
   __shared__ __attribute__((aligned(16))) float seg_o[SMAX][RR][68];
   __shared__ __attribute__((aligned(16))) T qs[XS_QP][16][72];
   __shared__ int s_ticket[2];
+  __shared__ int s_wnr[XS_QP], s_wr0[XS_QP];  // the range's pairs' window rows / first row, for the merge
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int r = lane & 15, g = lane >> 4;
   const int nseg = npair * nsp, nwg = gridDim.x, b = blockIdx.x;
@@ -1647,6 +1648,10 @@ __global__ __launch_bounds__(512, 1) void k_xattn_seg(const T* __restrict__ q, i
 #pragma unroll
   for (int pass = 0; pass < NQP; ++pass) {
     const int t = tid & 255;
+    if (t == 0) {  // kept for the merge (LDS, behind the staging barrier): no global round trip there
+      s_wnr[2 * pass + (tid >> 8)] = q_nr[pass];
+      s_wr0[2 * pass + (tid >> 8)] = q_r0[pass];
+    }
     const int qq = min(t >> 4, q_nr[pass] - 1), c = q_hj[pass] * 64 + (t & 15) * 4, row = q_r0[pass] + qq;
     if constexpr (QP) {
       const S* src = reinterpret_cast<const S*>(xq.part) + (int64_t)row * ldq + c;
@@ -1714,12 +1719,12 @@ __global__ __launch_bounds__(512, 1) void k_xattn_seg(const T* __restrict__ q, i
   const int part = tid / (RR * 16), t = tid - part * (RR * 16), qq = t >> 4, dc = (t & 15) * 4;
   auto emit = [&](int pj, const float4_t& o) {
     const int wj = pj / H, hj = pj - wj * H;
-    store4(out + (int64_t)(win_row0[wj] + qq) * ldo + hj * 64 + dc, o[0], o[1], o[2], o[3]);
+    store4(out + (int64_t)(s_wr0[pj - pa] + qq) * ldo + hj * 64 + dc, o[0], o[1], o[2], o[3]);
   };
 #pragma unroll
   for (int pass = 0; pass < (XS_QP + PPASS - 1) / PPASS; ++pass) {
     const int pj = pa + pass * PPASS + part;
-    if (pj <= plast && qq < win_nrows[pj / H]) {
+    if (pj <= plast && qq < s_wnr[pj - pa]) {
       const int l0 = pj * nsp - s0, l1 = l0 + nsp;  // the pair's tiles as local slots
       if (l0 >= 0 && l1 <= cnt) {                   // whole here: merge from LDS
         emit(pj, xs_merge(nsp, [&](int k, float& m, float& l, float4_t& o) {
@@ -1759,7 +1764,7 @@ __global__ __launch_bounds__(512, 1) void k_xattn_seg(const T* __restrict__ q, i
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // no instruction: keeps the loads below the add
   const int pj = part ? plast : pa;
   if (t == 0) __hip_atomic_store(xq.split_cnt + pj, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  if (qq >= win_nrows[pj / H]) return;  // only the window's rows were recorded
+  if (qq >= s_wnr[pj - pa]) return;  // only the window's rows were recorded
   emit(pj, xs_merge(nsp, [&](int k, float& m, float& l, float4_t& o) {
          const int rb = (pj * nsp + k) * XREC * 4;
          m = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, rb + (1024 + qq) * 4, 0, 16));
