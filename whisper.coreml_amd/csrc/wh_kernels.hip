@@ -374,17 +374,18 @@ __global__ __launch_bounds__(64) void k_self_attn(const T* __restrict__ q, int l
   __shared__ float sc[512];
   __shared__ int slot_of[512];
   const int row = blockIdx.x, h = blockIdx.y, lane = threadIdx.x;
+  // the query row leaves first, one element per lane (a vector load: a uniform-address
+  // load compiled to scalar loads that the compiler sank behind the ancestry's round trip);
+  // the fp16 path reads it from LDS (qs), the others unpack it into registers (qv)
+  __shared__ float qs[64];
+  const T q_lane = q[(int64_t)row * ldq + h * 64 + lane];
   const int w = row_win[row], sl = row_slot[row], pos = row_pos[row];
   const int* an = anc + ((int64_t)w * anc_beams + sl) * ctx;
   float qv[64];
-  {
-    const T* qr = q + (int64_t)row * ldq + h * 64;
+  auto unpack_q = [&] {  // (after qs is written and its lgkmcnt drained)
 #pragma unroll
-    for (int c = 0; c < 64; c += 4) {
-      const float4_t t = load4f(qr + c);
-      qv[c] = t[0]; qv[c + 1] = t[1]; qv[c + 2] = t[2]; qv[c + 3] = t[3];
-    }
-  }
+    for (int c = 0; c < 64; ++c) qv[c] = qs[c];
+  };
   const int64_t head_stride = (int64_t)ctx * 64;
   const int64_t wbase = (int64_t)w * nbeam;
   auto kv_off = [&](int slot, int p) -> int64_t { return ((wbase + slot) * H + h) * head_stride + (int64_t)p * 64; };
@@ -399,12 +400,14 @@ __global__ __launch_bounds__(64) void k_self_attn(const T* __restrict__ q, int l
     int sv[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) sv[i] = an[min(lane + 64 * i, ctx - 1)];
+    qs[lane] = to_f32(q_lane);
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       const int pp = lane + 64 * i;
       if (pp <= pos) slot_of[pp] = (pp == pos ? sl : sv[i]) * slotB;
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // one wave: its own LDS writes
+    unpack_q();
     const int kg = lane >> 3, dc = (lane & 7) * 8;
     float m = -INFINITY, lsum = 0.f, o[8];
 #pragma unroll
@@ -478,6 +481,7 @@ __global__ __launch_bounds__(64) void k_self_attn(const T* __restrict__ q, int l
     int sv[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) sv[i] = an[min(lane + 64 * i, ctx - 1)];
+    qs[lane] = to_f32(q_lane);
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       const int pp = lane + 64 * i;
@@ -504,12 +508,16 @@ __global__ __launch_bounds__(64) void k_self_attn(const T* __restrict__ q, int l
       __builtin_amdgcn_sched_barrier(0);  // every load of the pass ahead of the math
       float sa = 0.f, sb = 0.f;
 #pragma unroll
-      for (int c = 0; c < 8; ++c)
+      for (int c = 0; c < 8; ++c) {
+        const float4_t q0 = *reinterpret_cast<const float4_t*>(&qs[8 * c]);
+        const float4_t q1 = *reinterpret_cast<const float4_t*>(&qs[8 * c + 4]);
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
-          sa += qv[8 * c + e] * to_f32(ka[c].v[e]);
-          sb += qv[8 * c + e] * to_f32(kb[c].v[e]);
+          const float qe = e < 4 ? q0[e] : q1[e - 4];
+          sa += qe * to_f32(ka[c].v[e]);
+          sb += qe * to_f32(kb[c].v[e]);
         }
+      }
       const bool va = p0 + lane <= pos, vb = p0 + 64 + lane <= pos;
       const float mp = wave_max(fmaxf(va ? sa : -INFINITY, vb ? sb : -INFINITY));
       const float mn = fmaxf(m, mp), scale = __expf(m - mn);
@@ -543,6 +551,9 @@ __global__ __launch_bounds__(64) void k_self_attn(const T* __restrict__ q, int l
     CT_END(CT_SELF_ATTN);
     return;
   }
+  qs[lane] = to_f32(q_lane);
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // one wave: its own LDS write
+  unpack_q();
   // scores: lane per key
   float mx = -INFINITY;
   for (int p = lane; p <= pos; p += 64) {
