@@ -45,7 +45,7 @@ ORDER = [(0, "qkv k_proj", ("X staged", "MFMA done")), (6, "self-attn (+qkv redu
          (7, "cross-attn k_xattn_seg", None), (1, "cross-out k_proj", ("X staged", "MFMA done")),
          (2, "fc1 k_proj", ("X staged", "MFMA done")), (5, "reduce+GELU", None),
          (3, "fc2 k_proj", ("X staged", "MFMA done")), (4, "resid+LN (final)", ("loads landed", None)),
-         (8, "vocab k_vocab_2p / k_vocab1", ("half 0 staged", "half 1 staged")), (9, "selection k_logit_part", ("row combine", "window merge")),
+         (8, "vocab k_vocab_2p / k_vocab1", ("epilogue start", "half 1 staged")), (9, "selection k_logit_part", ("row combine", "window merge")),
          (10, "  merge_window (in it)", ("staged", "ranked")),
          (11, "  selection slices (marks)", ("loads", "top-k"))]
 

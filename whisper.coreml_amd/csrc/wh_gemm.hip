@@ -659,9 +659,13 @@ __global__ __launch_bounds__(512) void k_vocab_small(GemmArgs a) {
           if (mt * 16 + r < RG && m < a.M) {
 #if WH_WT
             const auto rs = wt_rsrc(a.out_f32);
+            if (n + 3 < a.N) {  // one 16-B store (k_vocab_2p's epilogue note)
+              wt_store4(rs, (m * a.ldo + n) * 4, acc[mt] + bv);
+            } else {
 #pragma unroll
-            for (int e = 0; e < 4; ++e)
-              if (n + e < a.N) wt_store1(rs, (m * a.ldo + n + e) * 4, acc[mt][e] + bv[e]);
+              for (int e = 0; e < 4; ++e)
+                if (n + e < a.N) wt_store1(rs, (m * a.ldo + n + e) * 4, acc[mt][e] + bv[e]);
+            }
 #else
             float* o = a.out_f32 + (int64_t)m * a.ldo;
 #pragma unroll
@@ -779,9 +783,13 @@ __global__ __launch_bounds__(512) void k_vocab1(GemmArgs a) {
 #pragma unroll
     for (int w = 1; w < KW; ++w) v += red[(tl * KW + w) * 64 + ln];
     if (rr < a.M) {
+      if (n + 3 < a.N) {
+        wt_store4(rs, (rr * a.ldo + n) * 4, v);  // one 16-B store (k_vocab_2p's epilogue note): 28.3 -> 27.0 us
+      } else {
 #pragma unroll
-      for (int e = 0; e < 4; ++e)
-        if (n + e < a.N) wt_store1(rs, (rr * a.ldo + n + e) * 4, v[e]);
+        for (int e = 0; e < 4; ++e)
+          if (n + e < a.N) wt_store1(rs, (rr * a.ldo + n + e) * 4, v[e]);
+      }
     }
   }
   CT_END(CT_VOCAB);
@@ -861,7 +869,7 @@ __global__ __launch_bounds__(1024) void k_vocab_2p(GemmArgs a) {
       }
     }
     __syncthreads();
-    CT_MARK(CT_VOCAB, 1 + h);  // this half of the rows staged
+    if (h) CT_MARK(CT_VOCAB, 2);  // the second half of the rows staged
     if (act) {
 #pragma unroll
       for (int c = 0; c < NCH; ++c) {
@@ -879,6 +887,7 @@ __global__ __launch_bounds__(1024) void k_vocab_2p(GemmArgs a) {
       }
     }
   }
+  CT_MARK(CT_VOCAB, 1);  // the MFMAs issued: the epilogue starts
   if (!act) {
     CT_END(CT_VOCAB);
     return;
@@ -895,8 +904,12 @@ __global__ __launch_bounds__(1024) void k_vocab_2p(GemmArgs a) {
     const int m = mt * 16 + r;
     if (m < a.M) {
       if (full) {
-#pragma unroll
-        for (int e = 0; e < 4; ++e) wt_store1(rs, (m * a.ldo + n + e) * 4, ov[mt][e]);
+        // the lane's 4 columns as ONE 16-B write-through store (whole 64-B row segments per
+        // instruction): four 4-B stores per element took the epilogue 15.5 us, this 7.5
+        // (k_vocab_2p 49.5 -> 41.6 us at 100 rows, profiles/r05/ab_vocab_wide_stores.txt;
+        // rows of the odd-width logit matrix start 8-B aligned: buffer stores take any
+        // dword-aligned address)
+        wt_store4(rs, (m * a.ldo + n) * 4, ov[mt]);
       } else {
 #pragma unroll
         for (int e = 0; e < 4; ++e)
