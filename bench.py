@@ -215,7 +215,7 @@ def load_traffic(kernel):
     """HBM bytes per launch of `kernel` from the committed PMC pass
     (profiles/<round>/traffic.json, written by profiles/pmc_traffic.py: FETCH_SIZE x2
     + WRITE_SIZE per the gfx950 correction of MI355X_MICROARCH.md), or None."""
-    for rnd in ("r04", "r03", "r02", "r01"):
+    for rnd in ("r05", "r04", "r03", "r02", "r01"):
         path = os.path.join(REPO, "profiles", rnd, "traffic.json")
         try:
             with open(path) as f:
