@@ -125,9 +125,10 @@ static __device__ unsigned long long g_ct_trace[CT_SLOTS][CT_WG][4];
 // which leaves every fp16 probability (min subnormal 2^-24) and every fp32 sum that
 // includes the row maximum's 1 unchanged.
 WH_DEV float hw_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
-// workgroup barrier for LDS data only: waits for this wave's LDS operations, not for its
-// global loads / stores in flight (__syncthreads waits vmcnt(0) too: a store round trip of
-// ~1-2 us when the wave has just written global memory nobody in the workgroup reads)
+// workgroup barrier for LDS data only: waits for this wave's LDS operations, never for its
+// global loads / stores in flight.  (__syncthreads is a workgroup-scope release + acquire;
+// hipcc decides per site whether that needs a vmcnt wait — in k_resid_ln it emits none,
+// in the fused selection it emitted some; this form does not depend on that choice.)
 WH_DEV void wh_lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 // floor(b * n / nb) of a contiguous range split (workgroup b of nb takes [split(b), split(b + 1))),
 // in 32-bit unsigned arithmetic: b * n < 2^32 at every call site (<= 256 workgroups x
