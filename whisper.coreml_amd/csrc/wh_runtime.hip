@@ -807,14 +807,19 @@ struct Ctx : public wh_ctx {
 
   // X[R][K] W^T into the split-K partial slabs part[z][R][N]: k_proj where a tile
   // configuration fits (decode rows <= 112), the k_gemv path otherwise; *ks = z
-  // Slabs are fp32.  WHISPER_HIP_SLAB16=1 (tuning build only) has k_proj store them as fp16
-  // (slab_h = 1 after such a partial()): at 20 windows it cut the step's summed kernel time
-  // by 0.3 % (profiles/r04/slab16_ab.txt), not worth fp16-rounded partial sums.
+  // fp16 contexts store the slabs as fp16 (slab_h = 1 after such a partial(); the QKV
+  // projection's stay fp32, read lane per element by the self-attention): half the bytes
+  // written by every k_proj and read by k_resid_ln / k_reduce_store / k_xattn_seg.  Round 4
+  // measured 0.3 % and kept fp32; after round 5's issue-side fixes the 20-window step graph
+  // is 3.378 -> 3.276 ms (early) and 3.661 -> 3.559 ms (150 tokens) with it
+  // (profiles/r05/ab_slab16.txt), the fp16 teacher-forced / invariance tests unchanged.
+  // Partial sums rounded to fp16 (the reference's CoreML path is fp16 end to end; the
+  // residual stream here stays fp32).  Tuning build: WHISPER_HIP_SLAB16=0 keeps fp32 slabs.
   int slab_h = 0;
   static bool slab16_enabled() {
     static const bool on = [] {
       const char* e = tune_env("WHISPER_HIP_SLAB16");
-      return e && e[0] == '1';
+      return !(e && e[0] == '0');
     }();
     return on;
   }
