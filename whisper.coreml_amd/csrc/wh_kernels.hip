@@ -655,8 +655,8 @@ void launch_self_attn(const T* q, int ldq, const T* kc, const T* vc, const int* 
 // the current pass is computed (two register buffers of 8 K + 8 V fragments), q read from
 // LDS: at long contexts the passes' round trips overlap instead of adding up (the step's
 // growth over the decode is those round trips, profiles/r04/self_attn_grp64_ab.txt).
-template <typename T, int PIPE = 0>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void k_self_attn_qkv(const float* __restrict__ part, int nsplit, int64_t part_stride,
+template <typename T, int PIPE = 0, typename S = float>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void k_self_attn_qkv(const S* __restrict__ part, int nsplit, int64_t part_stride,
                                                       const float* __restrict__ bqkv, int ns, T* __restrict__ kc,
                                                       T* __restrict__ vc, const int* __restrict__ row_win,
                                                       const int* __restrict__ row_slot, const int* __restrict__ row_pos,
@@ -690,24 +690,36 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void
   for (int i = 0; i < 8; ++i) sv[i] = an[min(lane + 64 * i, ctx - 1)];
   float qd, kd, vd;
   {
-    const float* pr = part + (int64_t)row * 3 * ns + h * 64 + lane;
-    float a0[16], a1[16], a2[16];
-#pragma unroll
-    for (int z = 0; z < 16; ++z)
-      if (z < nsplit) {
-        a0[z] = pr[z * part_stride];
-        a1[z] = pr[z * part_stride + ns];
-        a2[z] = pr[z * part_stride + 2 * ns];
-      }
+    // fp16 slabs: all 16 slab indices loaded unconditionally (clamped to the last split:
+    // the same addresses again), converted after every load is issued — guarded per split,
+    // the compiler converted each fp16 element inside its branch and waited there
+    constexpr bool H16 = sizeof(S) == 2;
+    const S* pr = part + (int64_t)row * 3 * ns + h * 64 + lane;
     qd = bqkv[h * 64 + lane];
     kd = bqkv[ns + h * 64 + lane];
     vd = bqkv[2 * ns + h * 64 + lane];
+    S a0[16], a1[16], a2[16];
+#pragma unroll
+    for (int z = 0; z < 16; ++z)
+      if (H16 || z < nsplit) {
+        const int64_t zo = (int64_t)(H16 ? min(z, nsplit - 1) : z) * part_stride;
+        a0[z] = pr[zo];
+        a1[z] = pr[zo + ns];
+        a2[z] = pr[zo + 2 * ns];
+      }
+    if constexpr (H16) {  // keeps the loads here (the compiler sank each into its split's sum,
+      // and the position's scalar load behind them all)
+      asm volatile("" ::"s"(pos));
+#pragma unroll
+      for (int z = 0; z < 16; ++z) asm volatile("" ::"v"(a0[z]), "v"(a1[z]), "v"(a2[z]));
+    }
+    auto f32 = [](S r) -> float { return (float)r; };
 #pragma unroll
     for (int z = 0; z < 16; ++z)
       if (z < nsplit) {
-        qd += a0[z];
-        kd += a1[z];
-        vd += a2[z];
+        qd += f32(a0[z]);
+        kd += f32(a1[z]);
+        vd += f32(a2[z]);
       }
   }
   for (int i = 0; i < 8; ++i)
@@ -1173,9 +1185,20 @@ int launch_self_attn_qkv(const float* part, int nsplit, int64_t part_stride, con
                           int ctx, T* out, int ldo, int rows, hipStream_t st, int slab_half) {
   if (rows <= 0) return 0;
   // the kernel takes window and beam from the row index: step rows are w * G + beam
-  // fp32 slabs only: the (row, head) wave reads its q / k / v columns lane per element
-  // (an fp16-slab form measured 8.7 -> 13.9 us per launch)
-  if (anc_beams < 1 || rows % anc_beams || nsplit > 16 || slab_half) return -1;
+  // fp16 slabs: the pipelined fp16 form only (round 4 measured an fp16-slab form of the
+  // 128-key kernel 8.7 -> 13.9 us per launch)
+  if (anc_beams < 1 || rows % anc_beams || nsplit > 16) return -1;
+  if (slab_half) {
+    if constexpr (sizeof(T) == 2) {
+      if (self_attn_pipe_on() && !self_attn_grp_mode()) {
+        k_self_attn_qkv<T, 1, half_t><<<rows * H, 64, 0, st>>>(reinterpret_cast<const half_t*>(part), nsplit,
+                                                              part_stride, bqkv, ns, kc, vc, rw, rs, rp, anc,
+                                                              anc_beams, nbeam, H, ctx, out, ldo), wh_launched("k_self_attn_qkv");
+        return 0;
+      }
+    }
+    return -1;
+  }
   // fp16 beams, tuning build only (WHISPER_HIP_SA_GRP=1): the grouped form, same arithmetic
   // per row.  Measured slower at every context length (20 windows: step 3.456 -> 3.655 ms
   // at 12 tokens, 3.834 -> 4.114 at 220, profiles/r04/self_attn_grp_ab.txt): at 238 VGPRs a

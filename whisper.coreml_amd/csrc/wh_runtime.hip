@@ -808,7 +808,7 @@ struct Ctx : public wh_ctx {
   // X[R][K] W^T into the split-K partial slabs part[z][R][N]: k_proj where a tile
   // configuration fits (decode rows <= 112), the k_gemv path otherwise; *ks = z
   // fp16 contexts store the slabs as fp16 (slab_h = 1 after such a partial(); the QKV
-  // projection's stay fp32, read lane per element by the self-attention): half the bytes
+  // projection's too when the self-attention is the pipelined fp16 form): half the bytes
   // written by every k_proj and read by k_resid_ln / k_reduce_store / k_xattn_seg.  Round 4
   // measured 0.3 % and kept fp32; after round 5's issue-side fixes the 20-window step graph
   // is 3.378 -> 3.276 ms (early) and 3.661 -> 3.559 ms (150 tokens) with it
@@ -819,6 +819,16 @@ struct Ctx : public wh_ctx {
   static bool slab16_enabled() {
     static const bool on = [] {
       const char* e = tune_env("WHISPER_HIP_SLAB16");
+      return !(e && e[0] == '0');
+    }();
+    return on;
+  }
+  // the QKV projection's slabs (read by k_self_attn_qkv's fp16 pipelined form) fp16 too:
+  // 20-window step graph 3.261 / 3.258 -> 3.255 / 3.246 ms, 3.557 -> 3.546 at 150 tokens
+  // (profiles/r05/ab_slab16_qkv.txt).  Tuning build: WHISPER_HIP_SLAB16_QKV=0 keeps them fp32
+  static bool slab16_qkv() {
+    static const bool on = [] {
+      const char* e = tune_env("WHISPER_HIP_SLAB16_QKV");
       return !(e && e[0] == '0');
     }();
     return on;
@@ -881,6 +891,7 @@ struct Ctx : public wh_ctx {
   // anc: the ancestry table the self-attention reads ([w][ancG][CTX]); the decode's S.anc
   // unless a first pass (alignment / prefill logits) gives its own (fp_anc: all zeros)
   int sa_probe_ks = 1;  // the QKV projection's split count (time_stage 8 / 9)
+  int sa_probe_half = 0;  // and whether its slabs were fp16
   int dec_layers(int R, const int* rw, const int* rs, const int* rp, int ancG, int nwin, const int* wr0, const int* wnr,
                  const int* wsl, float* aqk, const int* qkmap, int qkrows, bool step = false,
                  const int* anc = nullptr) {
@@ -898,8 +909,9 @@ struct Ctx : public wh_ctx {
       auto& e = dec[l];
       if (skinny) {
         int ks = 0;
-        TRY(partial(xn_d, n, e.wqkv, R, 3 * n, n, &ks, false));  // k_self_attn_qkv reads fp32 slabs
+        TRY(partial(xn_d, n, e.wqkv, R, 3 * n, n, &ks, slab16_qkv() && self_attn_pipe_on() && !self_attn_grp_mode()));
         sa_probe_ks = ks;
+        sa_probe_half = slab_h;
         if (launch_self_attn_qkv<T>(part, ks, (int64_t)R * 3 * n, e.bqkv, n, kc[l], vc[l], rw, rs, rp, A, ancG,
                                     Gcap, nh, CTX, att_d, n, R, st, slab_h))
           return fail(-20, "self-attention rows are not a whole number of beam groups");
@@ -1828,7 +1840,7 @@ struct Ctx : public wh_ctx {
       for (int i = 0; rc == 0 && i < iters; ++i)
         for (int l = 0; rc == 0 && l < Ld; ++l)
           if (launch_self_attn_qkv<T>(part, sa_probe_ks, (int64_t)R * 3 * n, dec[l].bqkv, n, kc[l], vc[l], st_row_win,
-                                      st_row_slot, row_pos, S.anc, cur_G, Gcap, nh, CTX, att_d, n, R, st, 0))
+                                      st_row_slot, row_pos, S.anc, cur_G, Gcap, nh, CTX, att_d, n, R, st, sa_probe_half))
             rc = fail(-20, "time_stage(8/9): self-attention launch refused");
       if (rc == 0 && hipEventRecord(tm.b, st) != hipSuccess) rc = fail(-100, "time_stage(8/9): hipEventRecord failed");
       if (saved) {
