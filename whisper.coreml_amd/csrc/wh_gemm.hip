@@ -835,13 +835,22 @@ __global__ __launch_bounds__(1024) void k_vocab_2p(GemmArgs a) {
   };
   constexpr int CPR = KH * 2 / 16;  // 16 B chunks per staged row
 #pragma unroll
-  for (int h = 0; h < 2; ++h) {
+  for (int hh = 0; hh < 2; ++hh) {
+#ifdef WH_VOCAB_SWAP  // probe build only (the k-step order decides the bits): second half of K
+    // first.  The first pass takes ~22 us and the second ~9 whichever half goes first
+    // (profiles/r05/vocab_pass_order.txt): an order effect, not a K-half one.  Pass 2's
+    // 66 MB in ~9 us (7.5 TB/s) is above any HBM rate measured here — consistent with (not
+    // proof of) pass 1 having pulled whole 2560-B rows into the Infinity Cache
+    const int h = 1 - hh;
+#else
+    const int h = hh;
+#endif
     // the pass's first DEPTH - 1 weight chunks ride with the staging loads
     if (act) {
 #pragma unroll
       for (int c = 0; c < DEPTH - 1 && c < NCH; ++c) load_chunk(h, c, wbuf[c]);
     }
-    if (h) __syncthreads();  // every wave is done with the first half's rows
+    if (hh) __syncthreads();  // every wave is done with the first half's rows
     if (xrows) {
       for (int c = tid; c < a.M * CPR; c += 1024) {
         const int row = c / CPR, col = c - row * CPR;
@@ -869,7 +878,7 @@ __global__ __launch_bounds__(1024) void k_vocab_2p(GemmArgs a) {
       }
     }
     __syncthreads();
-    if (h) CT_MARK(CT_VOCAB, 2);  // the second half of the rows staged
+    if (hh) CT_MARK(CT_VOCAB, 2);  // the second half of the rows staged
     if (act) {
 #pragma unroll
       for (int c = 0; c < NCH; ++c) {
