@@ -563,8 +563,11 @@ __device__ __forceinline__ void merge_window(const DecState& s, const DecOpts& o
 // per row) merges the kept slices.  Same choices as k_logit_rows; the normaliser is
 // summed per slice (float rounding of the log-probabilities differs in the last bits).
 constexpr int LP_THREADS = 512;
-// WH_LP_OCC=1: cap k_logit_part at 80 VGPRs (6 waves per SIMD: 3 workgroups per CU)
-#if defined(WH_LP_OCC) && WH_LP_OCC
+// WH_LP_OCC=1: cap k_logit_part at 80 VGPRs (6 waves per SIMD: 3 workgroups per CU);
+// WH_LP_OCC=2 (probe build): at 64 (8 waves per SIMD: 4 workgroups per CU)
+#if defined(WH_LP_OCC) && WH_LP_OCC == 2
+#define WH_LP_ATTR __attribute__((amdgpu_waves_per_eu(8)))
+#elif defined(WH_LP_OCC) && WH_LP_OCC
 #define WH_LP_ATTR __attribute__((amdgpu_waves_per_eu(6, 8)))
 #else
 #define WH_LP_ATTR
