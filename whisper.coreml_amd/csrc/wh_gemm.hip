@@ -806,7 +806,7 @@ __global__ __launch_bounds__(512) void k_vocab1(GemmArgs a) {
 // VC k-steps, the next chunk in flight while one is multiplied.  Accumulation runs over the
 // k-steps in ascending order into one accumulator per 16 x 16 block, as in k_vocab_small and
 // k_gemv_x: a row's logits are bit-identical whichever kernel the batch size selects.
-template <int MT, int DEPTH>
+template <int MT, int DEPTH, bool TR = false>
 __global__ __launch_bounds__(1024) void k_vocab_2p(GemmArgs a) {
   CT_MARK(CT_VOCAB, 0);
   constexpr int NW = 16, VC = DEPTH > 2 ? 4 : 5, KH = 640, SH = KH / 32, NCH = SH / VC;  // K 1280 (launcher)
@@ -897,6 +897,37 @@ __global__ __launch_bounds__(1024) void k_vocab_2p(GemmArgs a) {
     }
   }
   CT_MARK(CT_VOCAB, 1);  // the MFMAs issued: the epilogue starts
+  if constexpr (TR) {
+    // the workgroup's tiles transposed through LDS (X is dead): each store instruction
+    // writes 1 KB of one logit row instead of 16 rows x 64 B (the per-lane form below:
+    // 7.5 us of epilogue at 100 rows, this ~3)
+    constexpr int OTW = NW * 16 + 4;  // floats per staged row (+4: rows 4 banks apart)
+    float* ot = reinterpret_cast<float*>(xs2);
+    __syncthreads();  // every wave is done with the rows of X
+    if (act) {
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) {
+        const int m = mt * 16 + r;
+        if (m < a.M) *reinterpret_cast<float4_t*>(ot + m * OTW + wave * 16 + 4 * g) = acc[mt];
+      }
+    }
+    __syncthreads();
+    const auto rs = wt_rsrc(a.out_f32);
+    const int c0 = t0 * 16, nc = min(t1 * 16, a.N) - c0, nc4 = (nc + 3) >> 2;
+    for (int i = tid; i < a.M * nc4; i += 1024) {
+      const int m = i / nc4, c = 4 * (i - m * nc4), n = c0 + c;
+      const float4_t v = *reinterpret_cast<const float4_t*>(ot + m * OTW + c);
+      if (c + 3 < nc) {
+        wt_store4(rs, (m * a.ldo + n) * 4, v);
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          if (c + e < nc) wt_store1(rs, (m * a.ldo + n + e) * 4, v[e]);
+      }
+    }
+    CT_END(CT_VOCAB);
+    return;
+  }
   if (!act) {
     CT_END(CT_VOCAB);
     return;
@@ -1199,6 +1230,11 @@ int launch_gemm_tiles(const GemmArgs& a, int epi, int tile_sel, hipStream_t st) 
       // profiles/r03/step_tail_ab.txt
       const char* de = tune_env("WHISPER_HIP_V2P_DEPTH");
       const bool d3 = !(de && de[0] == '2');
+      // the epilogue through LDS, one 1-KB row segment per store instruction: 41.7 / 42.0 ->
+      // 37.4 / 37.4 us at 100 rows, step graph 3.244 / 3.251 -> 3.237 / 3.238 ms
+      // (profiles/r05/ab_vocab_epilogue_lds.txt).  Tuning: WHISPER_HIP_V2P_TR=0 -> per lane
+      const char* te = tune_env("WHISPER_HIP_V2P_TR");
+      const bool tr = !(te && te[0] == '0');
       const int nt = (a.N + 15) / 16;
       const int grid = std::max((nt + 15) / 16, std::min(256, nt));
       const int lds = a.M * (a.K + 16);  // rows x (K / 2 halves x 2 B + 16)
@@ -1209,6 +1245,13 @@ int launch_gemm_tiles(const GemmArgs& a, int epi, int tile_sel, hipStream_t st) 
                            hipFuncSetAttribute(reinterpret_cast<const void*>(&k_vocab_2p<MTV, 3>),
                                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) == hipSuccess;
         if (!attr) return -5;
+        if (tr) {  // the LDS-transposed epilogue (needs the staged rows' LDS: M x 1 KB + pad)
+          static bool attr_t = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_vocab_2p<MTV, 3, true>),
+                                                   hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) == hipSuccess;
+          if (!attr_t) return -5;
+          k_vocab_2p<MTV, 3, true><<<grid, 1024, std::max(lds, a.M * (16 * 16 + 4) * 4), st>>>(a), wh_launched("k_vocab_2p");
+          return 0;
+        }
         if (d3) k_vocab_2p<MTV, 3><<<grid, 1024, lds, st>>>(a), wh_launched("k_vocab_2p");
         else k_vocab_2p<MTV, 2><<<grid, 1024, lds, st>>>(a), wh_launched("k_vocab_2p");
         return 0;
