@@ -73,6 +73,9 @@ def parse():
                         "in a collective")
     p.add_argument("--dist-timeout", type=float, default=900.0,
                    help="seconds before a torch.distributed collective gives up")
+    p.add_argument("--balance", default="clips", choices=("clips", "tokens"),
+                   help="clips per rank: contiguous blocks (clips: equal clip counts, fixed work) or every N-th clip "
+                        "(tokens: natural decoding, where EOTs and speech density make windows unequal)")
     return p.parse_args()
 
 
@@ -148,8 +151,29 @@ def dist_setup(args):
     return world, rank, local, pg
 
 
+def parallelism_label(world, file_seconds, balance):
+    """config.parallelism: what the run's ranks exchange (nothing at world 1)."""
+    if world == 1:
+        return (f"one {file_seconds:.0f} s file on 1 GPU by 30 s clips (whisper/distributed.py, world 1: "
+                f"no collective runs)")
+    return (f"one {file_seconds:.0f} s file sharded over {world} GPUs by 30 s clips "
+            f"({'contiguous blocks' if balance == 'clips' else 'every ' + str(world) + '-th clip'}, "
+            f"whisper/distributed.py): RCCL all-reduce(max) of the log-mel maximum + gather of the segment records")
+
+
+def per_rank_report(pg, rec):
+    """Every rank's record (wall time, windows, tokens, time in the two collectives) on
+    every rank, in rank order: the N > 1 line shows why a scaling curve bends."""
+    if pg is None:
+        return [rec]
+    out = [None] * pg.get_world_size()
+    pg.all_gather_object(out, rec)
+    return out
+
+
 def launch_check(args):
-    """--launch-check 1: the ranks came up; rank 0 prints every rank's (rank, world)."""
+    """--launch-check 1: the ranks came up; rank 0 prints every rank's (rank, world) and
+    the per-rank record the bench line carries (no GPU work: times are zero)."""
     world, rank, _, pg = dist_setup(args)
     seen = [(rank, world)]
     if pg is not None and rank == args.launch_check_fail_rank:
@@ -157,8 +181,13 @@ def launch_check(args):
     if pg is not None:
         seen = [None] * world
         pg.all_gather_object(seen, (rank, pg.get_world_size()))
+    per_rank = per_rank_report(pg, dict(rank=rank, wall_s=0.0, windows=0, tokens=0, global_max_s=0.0, gather_s=0.0))
     if rank == 0:
-        print(json.dumps({"launch_check": True, "n_gpus": world, "ranks": seen}), flush=True)
+        line = {"launch_check": True, "n_gpus": world, "ranks": seen,
+                "parallelism": parallelism_label(world, 600.0 * world, args.balance)}
+        if world > 1:
+            line["per_rank"] = per_rank
+        print(json.dumps(line), flush=True)
     if pg is not None:
         pg.destroy_process_group()
 
@@ -343,21 +372,32 @@ def main():
     dev_audio = model.ctx.audio_upload(audio)
     decode_kw = dict(temperature=0.0, beam_size=args.beam, language="en")
 
+    # per-rank accounting of the timed steps (the N > 1 line's per_rank records)
+    acct = dict(global_max_s=0.0, gather_s=0.0, windows=0, tokens=0)
+
     def one_step():
         if args.word_timestamps:
             # config 5 on one GPU: the same clip grid, words aligned on the GPU per window
             clip_ts = ",".join(f"{30 * i},{30 * (i + 1)}" for i in range(n_clips))
             return whisper.transcribe(model, dev_audio, condition_on_previous_text=False, clip_timestamps=clip_ts,
                                       schedule="batched", word_timestamps=True, **decode_kw)["segments"]
-        st = D.prepare_shard(model, dev_audio, rank, world)
+        st = D.prepare_shard(model, dev_audio, rank, world, args.balance)
+        t = time.perf_counter()
         g = allreduce_max(pg, st.local_max)
-        segs = D.run_shard(model, st, g, **decode_kw)
+        acct["global_max_s"] += time.perf_counter() - t
+        segs = D.run_shard(model, st, g, balance=args.balance, **decode_kw)
+        acct["windows"] += len(st.clips)
+        acct["tokens"] += sum(len(s["tokens"]) for s in segs)
         if pg is None:
             return D.merge_segments([segs])
-        return D.gather_segments(segs)  # rank 0: the merged file; others: None
+        t = time.perf_counter()
+        merged = D.gather_segments(segs)  # rank 0: the merged file; others: None
+        acct["gather_s"] += time.perf_counter() - t
+        return merged
 
     for _ in range(args.warmup):
         one_step()
+    acct.update(global_max_s=0.0, gather_s=0.0, windows=0, tokens=0)
     barrier(pg)
     model.ctx.sync()
     st0 = model.ctx.stats()
@@ -371,6 +411,9 @@ def main():
     elapsed = time.perf_counter() - t0
     st1 = model.ctx.stats()
     elapsed_max = allreduce_max(pg, elapsed)
+    per_rank = per_rank_report(pg, dict(rank=rank, wall_s=round(elapsed, 4), windows=acct["windows"],
+                                        tokens=acct["tokens"], global_max_s=round(acct["global_max_s"], 5),
+                                        gather_s=round(acct["gather_s"], 5)))
     merged = results[-1]
 
     if args.dump and rank == 0:
@@ -461,8 +504,7 @@ def main():
     lv3 = args.model == "large-v3"
     traffic = load_traffic(kern["proj"]) if lv3 and (p1 or n_win == 20) else None
     xattn_traffic = load_traffic(kern["xattn"]) if lv3 and n_win == 20 else None
-    parallel = (f"one {file_seconds:.0f} s file sharded over {world} GPU(s) by 30 s clips (whisper/distributed.py): "
-                f"RCCL all-reduce(max) of the log-mel maximum + gather of the segment records")
+    parallel = parallelism_label(world, file_seconds, args.balance)
     out = {
         "metric": "xRT (audio-s/s) large-v3 beam=5 @1/2/4/8 GPU; p50 per-token decode ms",
         "value": round(file_seconds * args.steps / elapsed_max, 3),
@@ -512,6 +554,11 @@ def main():
     }
     if latency:
         out["latency_1window"] = latency
+    if world > 1:
+        # per rank over the timed steps: wall time, windows and segment tokens decoded, and
+        # the seconds spent in the two collectives (all-reduce MAX, segment gather)
+        out["per_rank"] = per_rank
+        out["balance"] = args.balance
     if verify is not None:
         out["verify"] = verify
     if rank == 0 and world == 1 and args.cpu_baseline and sd is not None:

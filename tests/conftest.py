@@ -11,6 +11,21 @@ for p in (PKG_ROOT, REPO):
 
 GOLDEN = os.path.join(REPO, "tests", "golden")
 
+# Every GPU run records each tolerance test's measured margin (worst relative error, where
+# it was, top-1 agreement, the bound it is held to) as one JSON line here, so a change that
+# ate most of a tolerance shows up even while the suite stays green (DESIGN.md §2;
+# profiles/summarize_margins.py folds a run's lines into profiles/<round>/fp16_margins.json).
+MARGIN_LOG = os.environ.get("WH_MARGIN_LOG", os.path.join(REPO, "gpurun_out", "margins.jsonl"))
+
+
+def record_margin(test, **fields):
+    import json
+    os.makedirs(os.path.dirname(MARGIN_LOG), exist_ok=True)
+    rec = {"test": test}
+    rec.update({k: (float(v) if hasattr(v, "dtype") and v.shape == () else v) for k, v in fields.items()})
+    with open(MARGIN_LOG, "a") as f:
+        f.write(json.dumps(rec) + "\n")
+
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (HIP device); run with -m gpu")

@@ -31,12 +31,26 @@ def test_launcher_brings_up_n_ranks(n):
     assert len(lines) == 1, p.stdout  # rank 0 only
     assert lines[0]["n_gpus"] == n
     assert sorted(map(tuple, lines[0]["ranks"])) == [(r, n) for r in range(n)]
+    # the per-rank records the N > 1 bench line carries, one per rank in rank order
+    pr = lines[0]["per_rank"]
+    assert [r["rank"] for r in pr] == list(range(n))
+    assert all(set(r) == {"rank", "wall_s", "windows", "tokens", "global_max_s", "gather_s"} for r in pr)
+    assert "RCCL all-reduce(max)" in lines[0]["parallelism"]
 
 
 def test_launcher_single_gpu_runs_in_process():
     p = _run(["--gpus", "1", "--launch-check", "1", "--backend", "gloo"])
     assert p.returncode == 0, p.stderr
-    assert _json_lines(p.stdout) == [{"launch_check": True, "n_gpus": 1, "ranks": [[0, 1]]}]
+    (line,) = _json_lines(p.stdout)
+    assert line["n_gpus"] == 1 and line["ranks"] == [[0, 1]] and "per_rank" not in line
+    assert "no collective" in line["parallelism"]
+
+
+def test_launcher_balance_tokens_label():
+    p = _run(["--gpus", "2", "--launch-check", "1", "--backend", "gloo", "--balance", "tokens"])
+    assert p.returncode == 0, p.stderr
+    (line,) = _json_lines(p.stdout)
+    assert "every 2-th clip" in line["parallelism"]
 
 
 def test_launcher_fails_when_a_rank_fails():

@@ -37,6 +37,40 @@ def test_shards_cover_every_clip_and_frame_once(seconds, world):
     assert all(a[1] == b[0] for a, b in zip(covered, covered[1:]))
 
 
+@pytest.mark.parametrize("seconds", [1.0, 65.0, 600.0, 3600.0])
+@pytest.mark.parametrize("world", [1, 2, 3, 8])
+@pytest.mark.parametrize("balance", D.BALANCES)
+def test_rank_clips_partition_and_frames(seconds, world, balance):
+    """Both balances deal every clip to exactly one rank; each rank's mel span holds its
+    clips, and the rank holding the last clip covers the padded tail (the max sees it)."""
+    n = int(seconds * 16000)
+    total = (n + N_SAMPLES) // HOP_LENGTH
+    grid = D.clip_grid(total - N_FRAMES)
+    dealt = []
+    spans = []
+    for r in range(world):
+        mine = D.rank_clips(len(grid), world, r, balance)
+        assert mine == sorted(mine)
+        dealt += mine
+        if mine:
+            f0, cnt = D.mel_frame_range(grid, mine[0], mine[-1] + 1, total, last=mine[-1] == len(grid) - 1)
+            spans.append((f0, f0 + cnt))
+            assert all(f0 <= grid[c][0] and grid[c][1] <= f0 + cnt for c in mine)
+    assert sorted(dealt) == list(range(len(grid)))
+    if balance == "tokens":
+        assert all(len(D.rank_clips(len(grid), world, r, balance)) in (len(grid) // world, -(-len(grid) // world))
+                   for r in range(world))
+    assert max(e for _, e in spans) == total and min(s for s, _ in spans) == 0
+
+
+def test_merge_interleaved_ranks_in_file_order():
+    a = [{"id": 0, "seek": 0}, {"id": 1, "seek": 0, "x": 1}, {"id": 2, "seek": 6000}]
+    b = [{"id": 0, "seek": 3000}, {"id": 1, "seek": 9000}]
+    m = D.merge_segments([a, b])
+    assert [s["seek"] for s in m] == [0, 0, 3000, 6000, 9000] and [s["id"] for s in m] == list(range(5))
+    assert m[1].get("x") == 1  # a window's segments keep their order
+
+
 def test_seconds_csv_round_trips_to_frames():
     grid = D.clip_grid(6500)
     ts = [float(x) for x in D.seconds_csv(grid).split(",")]

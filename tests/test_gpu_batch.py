@@ -22,7 +22,7 @@ import os
 import numpy as np
 import pytest
 
-from conftest import GOLDEN, full_model, golden_window
+from conftest import GOLDEN, full_model, golden_window, record_margin
 
 pytestmark = pytest.mark.gpu
 
@@ -203,6 +203,10 @@ def _teacher_forced_case(name, dtype, kind, n_win, mixed=False):
     print(f"{name} {dtype} {kind} rows={rel.shape[1]}{' mixed' if mixed else ''}: max rel err {rel.max():.3e} at step "
           f"{worst[0]} row {worst[1]}, p99 {np.quantile(rel, 0.99):.3e}, mean {rel.mean():.3e}; "
           f"top-1 agreement {top1.mean():.4f}")
+    record_margin("teacher_forced", model=name, dtype=dtype, kind=kind, windows=n_win, rows=int(rel.shape[1]),
+                  mixed=mixed, worst_rel=float(rel.max()), worst_step=int(worst[0]), worst_row=int(worst[1]),
+                  p99_rel=float(np.quantile(rel, 0.99)), mean_rel=float(rel.mean()), tau=TAU[dtype],
+                  frac_of_tau=float(rel.max() / TAU[dtype]), top1_agreement=float(top1.mean()))
     assert rel.max() <= TAU[dtype], f"max rel err {rel.max():.3e} > {TAU[dtype]}"
     assert top1.all(), f"top-1 differs at {np.argwhere(~top1)[:5].tolist()} despite a decisive margin"
     # every window of the batch is held to the bound on its own

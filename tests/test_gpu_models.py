@@ -17,7 +17,7 @@ import os
 import numpy as np
 import pytest
 
-from conftest import GOLDEN
+from conftest import GOLDEN, record_margin
 
 pytestmark = pytest.mark.gpu
 
@@ -53,6 +53,9 @@ def test_first_step_logits(name, dtype):
     rng = float(topv.max() - topv.min())
     err = float(np.abs(row[topi] - topv).max())
     print(f"{name} {dtype}: top-64 max abs err {err:.3e} (range {rng:.2f})")
+    bound = 1e-3 if dtype == "fp32" else 0.02
+    record_margin("first_step_logits", model=name, dtype=dtype, worst_rel=err / rng, tau=bound,
+                  frac_of_tau=err / rng / bound, top1_equal=bool(int(np.argmax(row)) == int(topi[0])))
     assert err < (1e-3 * rng if dtype == "fp32" else 0.02 * rng)
     assert int(np.argmax(row)) == int(topi[0])
     assert len(set(np.argsort(-row)[:5]) & set(topi[:5])) >= 4
@@ -119,6 +122,9 @@ def test_prompt_prefill_logits(name, dtype):
     rng = float(topv.max() - topv.min())
     err = float(np.abs(row[topi] - topv).max())
     print(f"{name} {dtype}: prompt prefill top-64 max abs err {err:.3e} (range {rng:.2f})")
+    bound = 1e-3 if dtype == "fp32" else 0.02
+    record_margin("prompt_prefill_logits", model=name, dtype=dtype, worst_rel=err / rng, tau=bound,
+                  frac_of_tau=err / rng / bound, top1_equal=bool(int(np.argmax(row)) == int(topi[0])))
     assert err < (1e-3 * rng if dtype == "fp32" else 0.02 * rng)
     assert int(np.argmax(row)) == int(topi[0])
 
@@ -143,6 +149,8 @@ def test_fp16_natural_greedy_agreement(name):
     n = min(len(got), len(ref))
     agree = int(np.argmax(got[:n] != ref[:n])) if np.any(got[:n] != ref[:n]) else n
     print(f"{name} fp16 natural greedy agreement {agree}/{len(ref)} (decisive prefix {need})")
+    record_margin("fp16_natural_greedy", model=name, dtype="fp16", agree_steps=agree, ref_steps=int(len(ref)),
+                  decisive_prefix=need, tokens_equal=bool(len(got) == len(ref) and np.array_equal(got, ref)))
     assert agree >= min(need, len(ref))
     if need >= len(margins):
         np.testing.assert_array_equal(got, ref)
@@ -165,5 +173,7 @@ def test_fp16_greedy_agreement(name):
     need = min(decisive_prefix(name, "greedy_fixed", TAU["fp16"]), len(ref))
     print(f"{name} fp16 greedy agreement {agree}/{len(ref)} (decisive prefix {need}); avg_logprob "
           f"{res.avg_logprob:.4f} vs {float(g['greedy_fixed_avg_logprob']):.4f}")
+    record_margin("fp16_fixed_greedy", model=name, dtype="fp16", agree_steps=agree, ref_steps=int(len(ref)),
+                  decisive_prefix=need, avg_logprob_diff=abs(float(res.avg_logprob) - float(g["greedy_fixed_avg_logprob"])))
     assert len(got) == len(ref)
     assert agree >= need

@@ -21,8 +21,10 @@ SECONDS = 3600.0
 WORLD = 8
 
 
-@pytest.mark.parametrize("dtype", ["fp16"])
-def test_config4_sharded_replay_equals_unsharded(dtype):
+@pytest.mark.parametrize("balance", ["clips", "tokens"])
+def test_config4_sharded_replay_equals_unsharded(balance, dtype="fp16"):
+    """balance "clips": contiguous 15-clip blocks; "tokens": every 8th clip per rank
+    (bench.py --balance tokens), merged back into file order by window seek."""
     import whisper
     from conftest import full_model
     from whisper import distributed as D
@@ -30,14 +32,14 @@ def test_config4_sharded_replay_equals_unsharded(dtype):
     m = full_model("large-v3", dtype)
     audio = S.synthetic_audio(SECONDS, seed=0)
     kw = dict(temperature=0.0, language="en", beam_size=5)
-    states = [D.prepare_shard(m, audio, r, WORLD) for r in range(WORLD)]
+    states = [D.prepare_shard(m, audio, r, WORLD, balance) for r in range(WORLD)]
     assert [len(s.clips) for s in states] == [15] * WORLD
     g = max(s.local_max for s in states)
-    per_rank = [D.run_shard(m, s, g, audio=audio, **kw) for s in states]
+    per_rank = [D.run_shard(m, s, g, audio=audio, balance=balance, **kw) for s in states]
     merged = D.merge_segments(per_rank)
     ref = whisper.transcribe(m, audio, condition_on_previous_text=False,
                              clip_timestamps=D.seconds_csv(D.clip_grid(int(SECONDS * 100))), **kw)["segments"]
-    print(f"config 4 replay: {len(merged)} segments sharded, {len(ref)} unsharded")
+    print(f"config 4 replay ({balance}): {len(merged)} segments sharded, {len(ref)} unsharded")
     assert len(merged) == len(ref)
     assert [s["seek"] for s in merged] == [s["seek"] for s in ref]
     assert [s["tokens"] for s in merged] == [s["tokens"] for s in ref]

@@ -247,6 +247,10 @@ def _compare_words(got, ref, label):
     prel = float(np.max(np.abs(gp - rp) / np.maximum(rp, 1e-6))) if len(rp) else 0.0
     print(f"{label}: {len(ref)} words, boundaries exact {exact:.4f}, within {WORD_TOL_S} s {near:.4f}, "
           f"max |d| {d.max() if len(d) else 0:.3f} s, max prob rel err {prel:.2e}")
+    from conftest import record_margin
+    record_margin("fp16_words", case=label, words=len(ref), exact_frac=exact, exact_bar=WORD_EXACT_FRAC,
+                  near_frac=near, near_bar=WORD_NEAR_FRAC, max_shift_s=float(d.max()) if len(d) else 0.0,
+                  prob_rel=prel, prob_bar=WORD_PROB_RTOL)
     return exact, near, prel
 
 
@@ -313,6 +317,8 @@ def test_large_v3_fp16_beam_word_timestamps(lv3_words):
         toks = [t for s in mine for t in s["tokens"]]
         agree = next((i for i, (a, b) in enumerate(zip(toks, r["tokens"])) if a != b), min(len(toks), len(r["tokens"])))
         print(f"window seek {r['seek']}: fp16 tokens agree with the reference for {agree}/{len(r['tokens'])}")
+        from conftest import record_margin
+        record_margin("fp16_beam_words_tokens", seek=int(r["seek"]), agree_tokens=int(agree), ref_tokens=len(r["tokens"]))
         if toks == r["tokens"]:
             same += 1
             exact, near, prel = _compare_words([w for s in mine for w in s["words"]], r["words"], f"seek {r['seek']}")

@@ -45,10 +45,31 @@ def shard_clips(n_clips: int, world: int, rank: int) -> Tuple[int, int]:
     return n_clips * rank // world, n_clips * (rank + 1) // world
 
 
+BALANCES = ("clips", "tokens")
+
+
+def rank_clips(n_clips: int, world: int, rank: int, balance: str = "clips") -> List[int]:
+    """Clip indices of ``rank``: a contiguous block (``balance="clips"``: equal clip
+    counts, the fixed-work case) or every world-th clip (``"tokens"``: natural decoding,
+    where a window's EOT ends its decode early and speech density drifts along a file,
+    so interleaved clips spread the long windows over the ranks)."""
+    if balance == "clips":
+        c0, c1 = shard_clips(n_clips, world, rank)
+        return list(range(c0, c1))
+    if balance == "tokens":
+        if not (0 <= rank < world):
+            raise ValueError(f"rank {rank} outside world {world}")
+        return list(range(rank, n_clips, world))
+    raise ValueError(f"balance must be one of {BALANCES}, not {balance!r}")
+
+
 def mel_frame_range(clips: Sequence[Tuple[int, int]], c0: int, c1: int, total_frames: int,
                     last: bool) -> Tuple[int, int]:
     """(frame0, count) of mel frames rank needs: its clips, plus — for the last rank —
-    every frame to the end of the padded file so the global max covers them all."""
+    every frame to the end of the padded file so the global max covers them all.
+    (Interleaved clips: c0 / c1 - 1 are the rank's first / last clip; the span covers the
+    clips between them, which other ranks decode — the log-mel is ~0.4 % of a window's
+    time, and MAX over overlapping spans is still the file's maximum.)"""
     if c1 <= c0:
         return 0, 0
     f0 = clips[c0][0]
@@ -72,7 +93,7 @@ class ShardState:
     local_max: float                      # -inf when the rank holds no frames
 
 
-def prepare_shard(model, audio, rank: int, world: int) -> ShardState:
+def prepare_shard(model, audio, rank: int, world: int, balance: str = "clips") -> ShardState:
     """Phase 1: this rank's mel frames and their (un-normalised) maximum."""
     from .backend_hip import DeviceAudio
     import numpy as np
@@ -86,16 +107,19 @@ def prepare_shard(model, audio, rank: int, world: int) -> ShardState:
     total = (n + N_SAMPLES) // HOP_LENGTH
     content = total - N_FRAMES
     grid = clip_grid(content)
-    c0, c1 = shard_clips(len(grid), world, rank)
-    f0, cnt = mel_frame_range(grid, c0, c1, total, last=rank == world - 1)
+    mine = rank_clips(len(grid), world, rank, balance)
+    # the rank that decodes the file's last clip also covers the padded tail (audio.py:145-146)
+    holds_last = bool(mine) and mine[-1] == len(grid) - 1
+    f0, cnt = mel_frame_range(grid, mine[0], mine[-1] + 1, total, last=holds_last) if mine else (0, 0)
     local_max = float("-inf")
     if cnt > 0:
         ctx.log_mel_frames(host, n, n_mels, f0, cnt, padding=N_SAMPLES, normalize=False)
         local_max = ctx.mel_max()
-    return ShardState(rank, world, n, total, grid[c0:c1], f0, cnt, local_max)
+    return ShardState(rank, world, n, total, [grid[c] for c in mine], f0, cnt, local_max)
 
 
-def run_shard(model, state: ShardState, global_max: float, audio=None, **transcribe_kw) -> List[dict]:
+def run_shard(model, state: ShardState, global_max: float, audio=None, balance: str = "clips",
+              **transcribe_kw) -> List[dict]:
     """Phase 2: normalise with the global max and transcribe this rank's clips
     (batched schedule).  ``audio`` re-supplies host audio when the context's mel
     buffer was reused by another shard since ``prepare_shard``."""
@@ -106,7 +130,7 @@ def run_shard(model, state: ShardState, global_max: float, audio=None, **transcr
     if not state.clips:
         return []
     if audio is not None:
-        prepare_again = prepare_shard(model, audio, state.rank, state.world)
+        prepare_again = prepare_shard(model, audio, state.rank, state.world, balance)
         assert prepare_again.frame0 == state.frame0 and prepare_again.count == state.count
     model.ctx.mel_normalize(global_max)
     kw = dict(transcribe_kw)
@@ -116,12 +140,12 @@ def run_shard(model, state: ShardState, global_max: float, audio=None, **transcr
 
 
 def merge_segments(per_rank: Sequence[Sequence[dict]]) -> List[dict]:
-    """Rank-ordered concatenation with ids renumbered (transcribe.py:468-480)."""
-    out = []
-    for segs in per_rank:
-        for s in segs:
-            out.append({**s, "id": len(out)})
-    return out
+    """The ranks' segments in file order with ids renumbered (transcribe.py:468-480): a
+    stable sort by window seek, so interleaved clips (balance "tokens") come back in clip
+    order and a window's segments keep their order (contiguous blocks are already sorted)."""
+    flat = [s for segs in per_rank for s in segs]
+    flat.sort(key=lambda s: s["seek"])
+    return [{**s, "id": i} for i, s in enumerate(flat)]
 
 
 def global_max(local: float, group=None) -> float:
