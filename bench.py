@@ -354,6 +354,12 @@ def main():
     from whisper import synthetic as S
 
     dims = S.MODEL_DIMS[args.model]
+    from whisper.backend_hip import max_windows_limit
+    lim = max_windows_limit(dims, args.dtype, args.beam)
+    if args.max_windows > lim:
+        print(f"bench.py: --max-windows {args.max_windows} exceeds what one context holds at beam {args.beam} in "
+              f"{args.dtype} (self-KV cache per layer < 2 GiB): using {lim}", file=sys.stderr, flush=True)
+        args.max_windows = lim
     sd = S.synthetic_state_dict(dims, 0)
     model = whisper.Whisper(whisper.ModelDimensions(**dims), args.model, device=local, dtype=args.dtype,
                             max_windows=args.max_windows, max_group=args.beam)

@@ -5,8 +5,17 @@ steps (WHISPER_HIP_EAGER=1, tuning library: rocprofv3 follows eager dispatches) 
 to ~205 tokens of context; `parse <fetch dir> <write dir>` reports the LAST step's 32
 self-attention dispatches (FETCH_SIZE x 2 gfx950 read correction, WRITE_SIZE exact) beside
 the logical K/V bytes (rows x heads x 2 x t x 64 x 2 B).
+
+Round 5's form (200 EAGER steps under `--pmc FETCH_SIZE --kernel-trace`) died with SIGSEGV
+inside the HIP launch path, in the profiler's interception of a k_proj dispatch, after
+~80 k dispatches (gpurun_out/sa_f.log): the same range in which rocprofv3's kernel trace
+crashes with trivial kernels (tools/graph_prof_repro.hip).  Round 6: the
+context is advanced by replaying the captured step graph (ADVANCE steps: no per-kernel host
+dispatch), then ONE eager step runs (the library reads WHISPER_HIP_EAGER per call), and the
+profiler counts only the self-attention (--kernel-include-regex), without --kernel-trace:
   cd /tmp && export TMPDIR=/tmp
-  WHISPER_HIP_EAGER=1 WHISPER_HIP_LIB=... rocprofv3 --pmc FETCH_SIZE --kernel-trace -d D -o run --output-format csv -- python sa_traffic.py run
+  WHISPER_HIP_LIB=... rocprofv3 --pmc FETCH_SIZE --kernel-include-regex k_self_attn_qkv -d D -o run \
+      --output-format csv -- python3 sa_traffic.py run
 """
 import csv
 import glob
@@ -31,7 +40,10 @@ def run():
     m.ctx.encode([3000 * i for i in range(20)], [3000] * 20)
     task = DecodingTask(m, whisper.DecodingOptions(language="en", beam_size=5))
     m.ctx.decode_begin(task.wh_opts(), [task.initial_tokens] * 20, [task.sot_index] * 20)
-    print("step ms", m.ctx.time_stage(0, STEPS), flush=True)
+    os.environ.pop("WHISPER_HIP_EAGER", None)
+    print("graph steps ms", m.ctx.time_stage(0, STEPS - 1), flush=True)  # context advanced in graph mode
+    os.environ["WHISPER_HIP_EAGER"] = "1"
+    print("eager step ms", m.ctx.time_stage(0, 1), flush=True)  # the traced step: 32 self-attention dispatches
     m.close()
 
 

@@ -31,15 +31,16 @@ lib = m.ctx.lib
 lib.wh_tune_xs_trace.restype = ctypes.c_int
 lib.wh_tune_xs_trace.argtypes = [ctypes.c_void_p]
 NAMES = ["start", "query staged", "wave 0 tiles done", "all tiles done", "merged / records drained",
-         "arrival counted", "cut pair merged"]
+         "arrival counted", "cut pair merged", "(qproj) X rows staged", "(qproj) W_q landed, MFMAs done"]
+NM = 10  # marks per workgroup (wh_kernels.hip XS_MARKS)
 for nw in wins:
     m.ctx.decode_begin(task.wh_opts(), [task.initial_tokens] * nw, [task.sot_index] * nw)
     m.ctx.time_stage(3, 1)
-    acc = {k: [] for k in range(7)}
+    acc = {k: [] for k in range(9)}
     spans = []
     for it in range(10):
         us_launch = m.ctx.time_stage(3, 1) * 1e3
-        buf = np.zeros((256, 8), dtype=np.uint64)
+        buf = np.zeros((256, NM), dtype=np.uint64)
         assert lib.wh_tune_xs_trace(buf.ctypes.data) == 0
         t = buf.astype(np.int64)
         live = t[:, 0] > 0
@@ -47,10 +48,10 @@ for nw in wins:
         live &= t[:, 0] >= t[live, 0].max() - 100000
         t = t[live]
         t0 = t[:, 0].min()
-        for k in range(7):
+        for k in range(9):
             col = t[:, k]
             ok = col >= t0
-            if k == 6:
+            if k >= 6:
                 ok &= col > 0
             if ok.any():
                 v = (col[ok] - t0) * 0.01
@@ -59,7 +60,7 @@ for nw in wins:
     sp = np.asarray(spans)
     print(f"windows {nw}: {len(t)} workgroups; launch (events, 32 layers) {np.median(sp[:, 0]):.2f} us, "
           f"first start -> last mark 5 {np.median(sp[:, 1]):.2f} us, last workgroup starts at {np.median(sp[:, 2]):.2f} us")
-    for k in range(7):
+    for k in range(9):
         if acc[k]:
             a = np.asarray(acc[k])
             print(f"  mark {k} {NAMES[k]:26s}: median {np.median(a[:, 0]):6.2f} us, max {np.median(a[:, 1]):6.2f} us "

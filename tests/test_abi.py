@@ -55,3 +55,17 @@ def test_load_model_without_checkpoint_raises(tmp_path):
     import whisper
     with pytest.raises(RuntimeError, match="not found"):
         whisper.load_model("large-v3", device=0, download_root=str(tmp_path))
+
+
+def test_context_refuses_self_kv_over_2gib_before_loading():
+    """One layer's self-KV cache must stay under 2 GiB (32-bit buffer offsets in the
+    self-attention kernels): the wrapper refuses a larger max_windows with the limit in the
+    message, before touching the library; bench.py clamps to the same limit."""
+    import pytest
+    from whisper import synthetic as S
+    from whisper.backend_hip import HipContext, max_windows_limit
+    d = S.MODEL_DIMS["large-v3"]
+    assert max_windows_limit(d, "fp32", 5) == 187 and max_windows_limit(d, "fp16", 5) == 374
+    assert (max_windows_limit(d, "fp32", 5) + 1) * 5 * 448 * 1280 * 4 >= (1 << 31) - 4096
+    with pytest.raises(ValueError, match="at most 187 windows"):
+        HipContext(d, dtype="fp32", max_windows=200, max_group=5)

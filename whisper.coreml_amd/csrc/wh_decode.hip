@@ -316,6 +316,9 @@ struct MergeLds {
   int etok[MG_MAXG];  // each row's input token for the next step
   float csc[MG_MAXG * KC];
   int csrc[MG_MAXG * KC], ctok[MG_MAXG * KC], rk[MG_MAXG * KC];
+  // k_logit_part<..., WIN>: the window's row combines leave their candidates here ([G][KC])
+  float wcv[MG_MAXG * KC];
+  int wci[MG_MAXG * KC];
 };
 // the next step's input rows of window w (k_embed's arithmetic: x = E[tok] + P[pos] in
 // fp32, pos = min(length - 1, pmax)); newtok[b]: row b's token at pos (passed from
@@ -353,7 +356,9 @@ __device__ void merge_embed(const MergeEmbed& em, int w, int G, int pos, const i
   else merge_embed_rows<float, NT>(em, w, G, pos, newtok, tid);
 }
 
-template <int NT, bool SC1>
+// LDSC: the candidates are in L.wcv / L.wci (the window's row combines ran in this
+// workgroup, k_logit_part<..., WIN>): no global round trip for them
+template <int NT, bool SC1, bool LDSC = false>
 __device__ __forceinline__ void merge_window(const DecState& s, const DecOpts& o, const MergeEmbed& em, int w, int tid, MergeLds& L) {
   static_assert(NT >= MG_MAXG * KC, "one lane per candidate");
   CT_MARK(CT_MERGE, 0);
@@ -373,11 +378,16 @@ __device__ __forceinline__ void merge_window(const DecState& s, const DecOpts& o
     return;
   }
   const auto rsv = wt_rsrc(s.cand_val), rsi = wt_rsrc(s.cand_idx);
-  auto cval = [&](int i) -> float {
+  // candidate k of row b of the window
+  auto cval = [&](int b, int k) -> float {
+    if constexpr (LDSC) return L.wcv[b * KC + k];
+    const int i = (w * G + b) * KC + k;
     if constexpr (SC1) return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsv, i * 4, 0, 16));
     else return s.cand_val[i];
   };
-  auto cidx = [&](int i) -> int {
+  auto cidx = [&](int b, int k) -> int {
+    if constexpr (LDSC) return L.wci[b * KC + k];
+    const int i = (w * G + b) * KC + k;
     if constexpr (SC1) return (int)__builtin_amdgcn_raw_buffer_load_b32(rsi, i * 4, 0, 16);
     else return s.cand_idx[i];
   };
@@ -385,9 +395,9 @@ __device__ __forceinline__ void merge_window(const DecState& s, const DecOpts& o
     if (tid < G) {
       const int r = w * G + tid;
       const int last = hist[tid * s.hctx + len - 1];
-      int t = cidx(r * KC);
+      int t = cidx(tid, 0);
       if (last == o.eot) t = o.eot;
-      else s.sum_lp[r] += cval(r * KC);
+      else s.sum_lp[r] += cval(tid, 0);
       hist[tid * s.hctx + len] = t;
       L.tok[tid] = t;
     }
@@ -431,8 +441,8 @@ __device__ __forceinline__ void merge_window(const DecState& s, const DecOpts& o
   const bool cl = tid < nc;  // nc <= MG_MAXG * KC = 72 <= NT
   if (cl) {
     const int b = tid / (G + 1), k = tid - b * (G + 1), r = w * G + b;
-    cs = s.sum_lp[r] + cval(r * KC + k);
-    ct = cidx(r * KC + k);
+    cs = s.sum_lp[r] + cval(b, k);
+    ct = cidx(b, k);
   }
 #pragma unroll
   for (int u = 0; u < MU; ++u) {
@@ -625,7 +635,8 @@ __device__ __forceinline__ void wave_argbest(float& v, int& idx) {
 }
 
 template <int NS, bool WT>
-__device__ __forceinline__ void lp_combine(const LPRec* rec, int r, const DecState& s, const DecOpts& o, int lane);
+__device__ __forceinline__ void lp_combine(const LPRec* rec, int r, const DecState& s, const DecOpts& o, int lane,
+                                           float* cv_out = nullptr, int* ci_out = nullptr);
 
 // Two barriers per workgroup: (1) after the history scan (last sampled timestamp), (2)
 // after every wave has reduced its own max, rescaled sum of exp and top-(G+1) list (or
@@ -638,11 +649,21 @@ __device__ __forceinline__ void lp_combine(const LPRec* rec, int r, const DecSta
 // workgroup, whose 8 waves then run the window's candidate merge (k_merge folded in:
 // merge_window<512, sc1 candidate loads>).  A finished window's rows are re-embedded by
 // its first row's first slice.
-template <int NS, int LP_EPT, bool FUSED, bool MERGE = false>
+//
+// WIN (with MERGE, round 6): the slices count on their WINDOW's counter (G x NS arrivals)
+// instead of their row's; the slice completing the window runs every row's combine in its
+// workgroup (wave b: row b's NS records, sc1 loads, then lp_combine into LDS) and the merge
+// reads those candidates from LDS — the row-level arrival, the candidates' write-through
+// stores, their drain and their sc1 reload leave the chain.  Same records, same combine
+// arithmetic, same merge: bit-identical selections.
+template <int NS, int LP_EPT, bool FUSED, bool MERGE = false, bool WIN = false>
 __global__ __launch_bounds__(LP_THREADS) WH_LP_ATTR void k_logit_part(float* __restrict__ logits, int ldl, DecState s,
                                                            DecOpts o, MergeEmbed em) {
   CT_MARK(CT_LOGIT, 0);
   static_assert(FUSED || !MERGE, "the merge rides on the fused combine");
+  static_assert(!WIN || MERGE, "window arrival: the merge runs in this launch");
+  // (WIN: the launcher checks that G x NS records fit the merge's history / ancestry
+  // staging, which they alias: lp_win_fits)
   constexpr int NWV = LP_THREADS / 64;
   __shared__ __attribute__((aligned(16))) char mlds_raw[MERGE ? sizeof(MergeLds) : 4];
   MergeLds& mlds = *reinterpret_cast<MergeLds*>(mlds_raw);
@@ -787,14 +808,53 @@ __global__ __launch_bounds__(LP_THREADS) WH_LP_ATTR void k_logit_part(float* __r
     if (lane == 0) __hip_atomic_store(s.lpw_cnt + w, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     return true;
   };
+  // WIN: the window's arrival (every slice of every row of window w); true for the last
+  auto arrive_window = [&]() -> bool {
+    CT_MARK(CT_LOGIT_SLICE, 2);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    int ticket = 0;
+    if (lane == 0) ticket = __hip_atomic_fetch_add(s.lpw_cnt + w, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    ticket = __shfl(ticket, 0, 64);
+    CT_MARK(CT_LOGIT_SLICE, 3);
+    if (ticket != s.G * NS - 1) return false;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // no instruction: keeps the loads below the add
+    if (lane == 0) __hip_atomic_store(s.lpw_cnt + w, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return true;
+  };
   // MERGE: wave 0 tells the workgroup whether it merges the window
   auto finish = [&](bool go) {
     if constexpr (MERGE) {
       if (wv == 0 && lane == 0) s_go = go;
       wh_lds_barrier();
       if (s_go) {
-        CT_MARK(CT_LOGIT, 2);  // this workgroup merges its window
-        merge_window<LP_THREADS, true>(s, o, em, w, tid, mlds);
+        if constexpr (WIN) {
+          CT_MARK(CT_LOGIT, 1);  // this workgroup combines the window's rows
+          // the rows' records alias the merge's history / ancestry staging (written after
+          // the barrier below); wave b combines row b (G <= MG_MAXG <= 8 waves)
+          float* wrec = reinterpret_cast<float*>(&mlds.oh[0][0]);
+          if (wv < s.G) {
+            const int rr = w * s.G + wv;
+            const auto rs = wt_rsrc(s.lpart + (int64_t)rr * LP_SLICES * LP_REC);
+            constexpr int N4 = NS * LP_REC / 4, PER = (N4 + 63) / 64;
+            float4_t v[PER];
+#pragma unroll
+            for (int k = 0; k < PER; ++k)
+              v[k] = __builtin_bit_cast(float4_t, __builtin_amdgcn_raw_buffer_load_b128(rs, min(lane + 64 * k, N4 - 1) * 16, 0, 16));
+            float* mine = wrec + wv * NS * LP_REC;
+#pragma unroll
+            for (int k = 0; k < PER; ++k)
+              if (lane + 64 * k < N4) reinterpret_cast<float4_t*>(mine)[lane + 64 * k] = v[k];
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // one wave: its own LDS writes
+            lp_combine<NS, false>(reinterpret_cast<const LPRec*>(mine), rr, s, o, lane, mlds.wcv + wv * KC,
+                                  mlds.wci + wv * KC);
+          }
+          wh_lds_barrier();
+          CT_MARK(CT_LOGIT, 2);  // this workgroup merges its window
+          merge_window<LP_THREADS, false, true>(s, o, em, w, tid, mlds);
+        } else {
+          CT_MARK(CT_LOGIT, 2);  // this workgroup merges its window
+          merge_window<LP_THREADS, true>(s, o, em, w, tid, mlds);
+        }
       }
     }
   };
@@ -873,7 +933,8 @@ __global__ __launch_bounds__(LP_THREADS) WH_LP_ATTR void k_logit_part(float* __r
         wt_rec(rec_off + offsetof(LPRec, gv), gv); wt_rec(rec_off + offsetof(LPRec, gi), __builtin_bit_cast(float, gi));
         wt_rec(rec_off + offsetof(LPRec, gx), gi != 0x7fffffff ? gx : -INFINITY);
       }
-      if constexpr (FUSED) go = arrive_and_combine();
+      if constexpr (WIN) go = arrive_window();
+      else if constexpr (FUSED) go = arrive_and_combine();
     } else {
       // beam: each lane holds up to two wave candidates (NWV * need <= 72), sorted within
       // the lane; `need` wave-level rounds take the best remaining head
@@ -897,7 +958,8 @@ __global__ __launch_bounds__(LP_THREADS) WH_LP_ATTR void k_logit_part(float* __r
         }
       }
       if (lane == 0) { wt_rec(rec_off + offsetof(LPRec, mx), MX); wt_rec(rec_off + offsetof(LPRec, se), SE); }
-      if constexpr (FUSED) go = arrive_and_combine();
+      if constexpr (WIN) go = arrive_window();
+      else if constexpr (FUSED) go = arrive_and_combine();
     }
   }  // wave 0
   finish(go);
@@ -908,8 +970,10 @@ __global__ __launch_bounds__(LP_THREADS) WH_LP_ATTR void k_logit_part(float* __r
 // selection between text and timestamps, the normaliser, then argbest / top-(G+1) with one
 // slice per lane (decoding.py:522-531 and the candidate lists of 707-733)
 // WT: the candidates are stored write-through (sc1), for the merge in the same launch
+// cv_out / ci_out (WT false): where the row's candidates go instead of s.cand_val / cand_idx
 template <int NS, bool WT>
-__device__ __forceinline__ void lp_combine(const LPRec* rec, int r, const DecState& s, const DecOpts& o, int lane) {
+__device__ __forceinline__ void lp_combine(const LPRec* rec, int r, const DecState& s, const DecOpts& o, int lane,
+                                           float* cv_out, int* ci_out) {
   constexpr int TS = NS - 1;
   float m = -INFINITY;
   for (int j = 0; j < NS; ++j) m = fmaxf(m, rec[j].mx);
@@ -932,8 +996,8 @@ __device__ __forceinline__ void lp_combine(const LPRec* rec, int r, const DecSta
   for (int j = j0; j < NS; ++j)
     if (rec[j].mx > -INFINITY) se += rec[j].se * __expf(rec[j].mx - m);
   const float logS = logf(se);
-  float* cv = s.cand_val + (int64_t)r * KC;
-  int* ci = s.cand_idx + (int64_t)r * KC;
+  float* cv = cv_out ? cv_out : s.cand_val + (int64_t)r * KC;
+  int* ci = ci_out ? ci_out : s.cand_idx + (int64_t)r * KC;
   // lane j holds slice j (NS <= 64): wave-level argbest rounds, the order of better()
   // (value desc, index asc) as in the slices themselves
   static_assert(NS <= 64 && NS <= LP_SLICES, "one lane per slice");
@@ -1024,6 +1088,14 @@ static bool select_rows(float* logits, int ldl, const DecState& s, const DecOpts
   }();
   const int rows = nwin * s.G;
   const bool merge = em && fold_merge && s.lpw_cnt && s.G <= MG_MAXG;
+  // the window-level arrival (k_logit_part<..., WIN>) unless WHISPER_HIP_LP_WIN=0 (tuning)
+  static const bool win_on = [] {
+    const char* e = tune_env("WHISPER_HIP_LP_WIN");
+    return !(e && e[0] == '0');
+  }();
+  auto lp_win_fits = [&](int ns) {
+    return win_on && (size_t)s.G * ns * LP_REC * 4 <= sizeof(MergeLds::oh) + sizeof(MergeLds::oa);
+  };
   const bool sp = split && s.hctx <= LP_THREADS;  // k_logit_part: one history position per thread
   const MergeEmbed none;
   const MergeEmbed& e = em ? *em : none;
@@ -1044,14 +1116,16 @@ static bool select_rows(float* logits, int ldl, const DecState& s, const DecOpts
   const bool one_win = nwin == 1;
   if (sp && fused && !one_win && ns_force == 16 && o.ts_begin > 0 &&
       (o.ts_begin + 14) / 15 <= LP_THREADS * 8 && o.V - o.ts_begin <= LP_THREADS * 8) {
-    if (merge) k_logit_part<16, 8, true, true><<<dim3(rows, 16), LP_THREADS, 0, st>>>(logits, ldl, s, o, e), wh_launched("k_logit_part");
+    if (merge && lp_win_fits(16)) k_logit_part<16, 8, true, true, true><<<dim3(rows, 16), LP_THREADS, 0, st>>>(logits, ldl, s, o, e), wh_launched("k_logit_part<win>");
+    else if (merge) k_logit_part<16, 8, true, true><<<dim3(rows, 16), LP_THREADS, 0, st>>>(logits, ldl, s, o, e), wh_launched("k_logit_part");
     else k_logit_part<16, 8, true><<<dim3(rows, 16), LP_THREADS, 0, st>>>(logits, ldl, s, o, e), wh_launched("k_logit_part");
     return merge;
   }
   if (sp && o.ts_begin > 0 && (one_win || ns_force == 32) && (o.ts_begin + 30) / 31 <= LP_THREADS * 4 &&
       o.V - o.ts_begin <= LP_THREADS * 4) {
     if (fused) {
-      if (merge) k_logit_part<32, 4, true, true><<<dim3(rows, 32), LP_THREADS, 0, st>>>(logits, ldl, s, o, e), wh_launched("k_logit_part");
+      if (merge && lp_win_fits(32)) k_logit_part<32, 4, true, true, true><<<dim3(rows, 32), LP_THREADS, 0, st>>>(logits, ldl, s, o, e), wh_launched("k_logit_part<win>");
+      else if (merge) k_logit_part<32, 4, true, true><<<dim3(rows, 32), LP_THREADS, 0, st>>>(logits, ldl, s, o, e), wh_launched("k_logit_part");
       else k_logit_part<32, 4, true><<<dim3(rows, 32), LP_THREADS, 0, st>>>(logits, ldl, s, o, e), wh_launched("k_logit_part");
       return merge;
     }

@@ -46,7 +46,17 @@ struct XQPart {
   float* split_rec = nullptr;
   int* split_cnt = nullptr;
   int max_pairs = 0;
+  // round 6: the query projected inside the step kernel (xattn_fused_q): q = qx qw^T + bias
+  // with qx the LayerNorm'd rows [rows][n] and qw = W_q [n][n] (T); q / part unused
+  const void* qx = nullptr;
+  const void* qw = nullptr;
 };
+// the shapes the in-kernel query projection serves: fp16, n = 1280 (large-v3, turbo), <= 8
+// rows per window; the choice depends on the model and the beam group only, never on the
+// window count (a window's step stays batch-invariant)
+inline bool xattn_fused_q(int n, int rows_per_window, int elem_size) {
+  return elem_size == 2 && n == 1280 && rows_per_window >= 1 && rows_per_window <= 8;
+}
 constexpr int XREC = 16 * 64 + 32;  // floats per segment record: O[16][64], m[16], l[16]
 // step cross-attention (k_xattn_seg): one softmax partial per 64-key tile, at most
 // XS_NSP tiles per (window, head) pair (Tk <= 1536), at most XS_QP pairs per workgroup

@@ -1540,7 +1540,7 @@ WH_DEV float4_t xs_merge(int n, Get get) {
 #if WH_TUNING
 // tuning build: per-workgroup wall-clock marks (s_memrealtime, 100 MHz) of the last
 // k_xattn_seg launch, read by wh_tune_xs_trace (profiles/xattn_trace.py)
-constexpr int XS_MARKS = 8;
+constexpr int XS_MARKS = 10;
 __device__ unsigned long long g_xs_trace[256][XS_MARKS];
 #define XS_MARK(k)                                                                         \
   do {                                                                                     \
@@ -1552,7 +1552,126 @@ __device__ unsigned long long g_xs_trace[256][XS_MARKS];
   } while (0)
 #endif
 
-template <typename T, int QZ, int RR, typename S = float, bool FULL = false>
+// Round 6: the decoder step's cross-attention query projected inside k_xattn_seg (QK > 0)
+// instead of by a split-K k_proj launch whose fp16 slabs the kernel summed: the range's
+// pairs (at most XS_QF: a range holds <= 2 x nsp tiles with nsp = 24) each need
+//   q[row][c] = (S0 + S1) + bias[c],  S_kh = sum over the K half kh of X[row][k] W_q[c][k]
+// (MFMA accumulation in k-step order; the two halves meet in LDS in that order), the
+// same arithmetic whichever workgroup, grid form or batch computes it (batch invariance).
+// The 8 waves are (16-column tile c of the head's 64, K half kh); a pair's window rows
+// (<= RR) are staged in LDS (rows past the window read 0 through the buffer limit: their
+// queries are never emitted), the wave's 16 x n / 2 slice of W_q (QK fragments) is loaded
+// once per head, and the first tile's K / V leave before the wait (clamped: no branch).
+// X is staged in the tile partials' LDS (dead until the first tile) and the halves' sum
+// goes through it too.  Reference: decoder.py:73-91 (cross-attention query), :42 (scale).
+constexpr int XS_QF = 3;
+template <typename T, int QK, int RR, typename PairWH, typename LoadKV>
+WH_DEV void xq_project(const XQPart& xq, int pa, int plast, int cnt, const int* __restrict__ win_row0,
+                       const int* __restrict__ win_nrows, PairWH pair_wh, LoadKV load_kv, Frag<T> (&kA)[4][2],
+                       Frag<T> (&vA)[4][2], char* xst, T (*qs)[16][72], int* s_wnr, int* s_wr0) {
+  static_assert(sizeof(T) == 2, "fused query projection: fp16 contexts");
+  constexpr int N = QK * 64;                           // model width = K
+  constexpr int CPR = N * (int)sizeof(T) / 16;         // 16-B chunks per row
+  constexpr int XROWB = N * (int)sizeof(T) + 16;       // padded LDS row (bytes)
+  constexpr int XPT = (RR * CPR + 511) / 512;          // chunks per thread per pair
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = lane & 15, g = lane >> 4;
+  const int c = wave & 3, kh = wave >> 2;
+  const int np = plast - pa + 1;
+  // the pairs' heads and window rows: scalar loads, one round trip
+  int q_h[XS_QF], q_nr[XS_QF], q_r0[XS_QF];
+#pragma unroll
+  for (int j = 0; j < XS_QF; ++j) {
+    const int pj = __builtin_amdgcn_readfirstlane(min(pa + j, plast));
+    int wj, hj;
+    pair_wh(pj, wj, hj);
+    q_h[j] = hj;
+    q_nr[j] = win_nrows[wj];
+    q_r0[j] = win_row0[wj];
+  }
+  // 1. each pair's window rows -> registers (unconditional loads; the buffer limit is the
+  // window's rows, 0 for pairs past the range)
+  float4_t xv[XS_QF][XPT];
+#pragma unroll
+  for (int j = 0; j < XS_QF; ++j) {
+    const auto rs = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<T*>(reinterpret_cast<const T*>(xq.qx)) + (int64_t)q_r0[j] * N, 0, j < np ? q_nr[j] * N * (int)sizeof(T) : 0,
+        0x00020000);
+#pragma unroll
+    for (int i = 0; i < XPT; ++i) {
+      const int ch = tid + 512 * i, off = (ch / CPR) * (N * (int)sizeof(T)) + (ch % CPR) * 16;
+      xv[j][i] = __builtin_bit_cast(float4_t, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0));
+    }
+  }
+  float4_t bq[XS_QF];
+#pragma unroll
+  for (int j = 0; j < XS_QF; ++j) bq[j] = load4f(xq.bias + q_h[j] * 64 + c * 16 + 4 * g);
+  // 2. the wave's W_q fragments for the first pair's head: rows h*64 + 16c + r, K half kh
+  Frag<T> wf[QK];
+  auto load_w = [&](int h) {
+    const T* wp = reinterpret_cast<const T*>(xq.qw) + (int64_t)(h * 64 + c * 16 + r) * N + kh * QK * 32 + 8 * g;
+#pragma unroll
+    for (int s = 0; s < QK; ++s) frag_load_stream(wf[s], wp + s * 32);
+  };
+  load_w(q_h[0]);
+  // 3. the first tile's K / V
+  load_kv(min(wave, cnt - 1), kA, vA);
+  __builtin_amdgcn_sched_barrier(0);
+  // 4. X -> LDS (waits for the X loads alone: they were issued first)
+#pragma unroll
+  for (int j = 0; j < XS_QF; ++j)
+#pragma unroll
+    for (int i = 0; i < XPT; ++i) {
+      const int ch = tid + 512 * i;
+      if (ch < RR * CPR)
+        *reinterpret_cast<float4_t*>(xst + (j * RR + ch / CPR) * XROWB + (ch % CPR) * 16) = xv[j][i];
+    }
+  if (tid == 0) {  // the merge's window rows (LDS, behind the barriers below)
+#pragma unroll
+    for (int j = 0; j < XS_QF; ++j) {
+      s_wnr[j] = q_nr[j];
+      s_wr0[j] = q_r0[j];
+    }
+  }
+  wh_lds_barrier();
+  XS_MARK(7);  // X staged
+  // 5. pair by pair: MFMAs in k-step order (W reloaded only where the head changes)
+  float4_t qa[XS_QF];
+#pragma unroll
+  for (int j = 0; j < XS_QF; ++j) {
+    qa[j] = (float4_t){0.f, 0.f, 0.f, 0.f};
+    if (j < np) {
+      if (j > 0 && q_h[j] != q_h[j - 1]) load_w(q_h[j]);
+      const char* xl = xst + (j * RR + min(r, RR - 1)) * XROWB + (kh * QK * 32 + 8 * g) * (int)sizeof(T);
+#pragma unroll
+      for (int s = 0; s < QK; ++s) {
+        Frag<T> xf;
+        frag_load(xf, reinterpret_cast<const T*>(xl + s * 32 * (int)sizeof(T)));
+        mfma_step(qa[j], wf[s], xf);
+      }
+    }
+  }
+  XS_MARK(8);  // this wave's (thread 0's) MFMAs done: its W_q fragments landed
+  // 6. the K halves meet (half 0 + half 1, then the bias) -> qs[pair][row][64] (fp16)
+  wh_lds_barrier();  // every wave's X reads are done: the area is reused
+  float4_t* red = reinterpret_cast<float4_t*>(xst);  // [XS_QF][4][64]
+  if (kh == 1) {
+#pragma unroll
+    for (int j = 0; j < XS_QF; ++j)
+      if (j < np) red[(j * 4 + c) * 64 + lane] = qa[j];
+  }
+  wh_lds_barrier();
+  if (kh == 0) {
+#pragma unroll
+    for (int j = 0; j < XS_QF; ++j)
+      if (j < np) {
+        float4_t v = qa[j] + red[(j * 4 + c) * 64 + lane];
+        v += bq[j];
+        store4(&qs[j][r][c * 16 + 4 * g], v[0], v[1], v[2], v[3]);
+      }
+  }
+}
+
+template <typename T, int QZ, int RR, typename S = float, bool FULL = false, int QK = 0>
 __global__ __launch_bounds__(512, 1) void k_xattn_seg(const T* __restrict__ q, int ldq, const T* ck, const T* cvt, int Tk,
                                                      int H, int npair, int nsp, const int* __restrict__ win_row0,
                                                      const int* __restrict__ win_nrows,
@@ -1560,6 +1679,11 @@ __global__ __launch_bounds__(512, 1) void k_xattn_seg(const T* __restrict__ q, i
                                                      T* __restrict__ out, int ldo) {
   constexpr int NW = 8, SMAX = XsShape<RR>::SMAX, PPASS = 512 / (RR * 16);  // pairs merged per pass
   constexpr bool QP = QZ > 0;
+  // QK > 0 (round 6): the query projection itself runs here (xq.qx rows x xq.qw^T + bias,
+  // QK k-steps per K half), pairs are numbered head-major (p = head * nwin + window: a
+  // workgroup's pairs share one head's 64 x n slice of W_q) and workgroups are laid over
+  // the XCDs in contiguous logical runs, so a head's slice crosses HBM about once per XCD
+  constexpr bool QF = QK > 0;
   __shared__ float seg_m[SMAX][RR], seg_l[SMAX][RR];
   // partial outputs row-major, 68-float rows: a lane's 4 columns are one 16-B store / load
   // (tile(): lanes r = 0..7 of a store group hit banks 4r.. +3, conflict-free; round 4 kept
@@ -1570,9 +1694,20 @@ __global__ __launch_bounds__(512, 1) void k_xattn_seg(const T* __restrict__ q, i
   __shared__ int s_wnr[XS_QP], s_wr0[XS_QP];  // the range's pairs' window rows / first row, for the merge
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int r = lane & 15, g = lane >> 4;
-  const int nseg = npair * nsp, nwg = gridDim.x, b = blockIdx.x;
+  const int nseg = npair * nsp, nwg = gridDim.x, b = QF ? xcd_remap(blockIdx.x, nwg) : (int)blockIdx.x;
   const int s0 = range_split(b, nseg, nwg), s1 = range_split(b + 1, nseg, nwg), cnt = s1 - s0;
   const int pa = s0 / nsp, plast = (s1 - 1) / nsp;
+  const int nwin = QF ? npair / H : 0;
+  // pair p -> (window, head)
+  auto pair_wh = [&](int p, int& wi, int& h) {
+    if constexpr (QF) {
+      h = p / nwin;
+      wi = p - h * nwin;
+    } else {
+      wi = p / H;
+      h = p - wi * H;
+    }
+  };
   XS_MARK(0);
   CT_MARK(CT_XATTN, 0);
 
@@ -1582,7 +1717,9 @@ __global__ __launch_bounds__(512, 1) void k_xattn_seg(const T* __restrict__ q, i
     // i is wave-uniform: the tile's window slot comes by a scalar load (lgkmcnt).  Round 4:
     // as a vector load it sat in vmcnt order, and the s_waitcnt vmcnt(0) before the K / V
     // addresses drained the tile in flight: one tile per wave in flight, not two
-    const int gs = __builtin_amdgcn_readfirstlane(s0 + i), p = gs / nsp, k = gs - p * nsp, wi = p / H, h = p - wi * H;
+    const int gs = __builtin_amdgcn_readfirstlane(s0 + i), p = gs / nsp, k = gs - p * nsp;
+    int wi, h;
+    pair_wh(p, wi, h);
     const int64_t off = (int64_t)(wsl >= 0 ? wsl : win_slot[wi]) * win_stride;
     const T* kbase = ck + off + (int64_t)h * TKP * 64;
     const T* vbase = cvt + off + (int64_t)h * 64 * TKP;
@@ -1659,6 +1796,12 @@ __global__ __launch_bounds__(512, 1) void k_xattn_seg(const T* __restrict__ q, i
   // burst is still landing (the query used to wait behind the whole first tile,
   // profiles/xattn_trace.py: query staged at 5.3 us of a 34 us launch at 20 windows)
   constexpr int NQP = XS_QP / 2;
+  if constexpr (QF) {
+    static_assert(XS_QF * RR * (QK * 64 * sizeof(T) + 16) <= sizeof(seg_o), "X rows in the partials' LDS");
+    static_assert(XS_QF * 4 * 64 * 16 <= sizeof(seg_o), "K-half sums in the partials' LDS");
+    xq_project<T, QK, RR>(xq, pa, plast, cnt, win_row0, win_nrows, pair_wh, load_kv, kA, vA,
+                          reinterpret_cast<char*>(&seg_o[0][0][0]), qs, s_wnr, s_wr0);
+  } else {
   // FULL (the launcher: every workgroup holds >= 8 tiles, one per wave at least): the order
   // above; otherwise (few windows, <= 1 tile per wave) the first tile leaves first, as the
   // query then has no second tile to overlap
@@ -1723,6 +1866,7 @@ __global__ __launch_bounds__(512, 1) void k_xattn_seg(const T* __restrict__ q, i
     __builtin_amdgcn_sched_barrier(0);
   }
   stage_q();
+  }
   asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // LDS only
   XS_MARK(1);
 
@@ -1752,7 +1896,8 @@ __global__ __launch_bounds__(512, 1) void k_xattn_seg(const T* __restrict__ q, i
   const auto rs = __builtin_amdgcn_make_buffer_rsrc(xq.split_rec, 0, 0x7fffffff, 0x00020000);
   const int part = tid / (RR * 16), t = tid - part * (RR * 16), qq = t >> 4, dc = (t & 15) * 4;
   auto emit = [&](int pj, const float4_t& o) {
-    const int wj = pj / H, hj = pj - wj * H;
+    int wj, hj;
+    pair_wh(pj, wj, hj);
     store4(out + (int64_t)(s_wr0[pj - pa] + qq) * ldo + hj * 64 + dc, o[0], o[1], o[2], o[3]);
   };
 #pragma unroll
@@ -1862,6 +2007,25 @@ void launch_cross_attn(const T* q, int ldq, const T* ck, const T* cv, int Tk, in
     // FULL: every workgroup's range holds >= 8 tiles (one per wave), e.g. 20 windows
     const int nwg_xs = xattn_seg_grid(npair, nsp, xq.max_rows <= 8 ? XsShape<8>::SMAX : XsShape<16>::SMAX);
     const bool full = (npair * nsp) / nwg_xs >= 8;
+    if (xq.qx) {  // the query projected in the kernel (round 6)
+      if constexpr (sizeof(T) == 2) {
+        if (!xq.qw || !xq.bias || !xattn_fused_q(H * 64, xq.max_rows, (int)sizeof(T)) || nsp != XS_NSP) {
+          wh_set_launch_error("launch_cross_attn: fused query projection outside its shapes");
+          return;
+        }
+        if (full)
+          k_xattn_seg<T, 0, 8, float, true, 20><<<nwg_xs, 512, 0, st>>>(q, ldq, ck, cv, Tk, H, npair, nsp, win_row0,
+                                                                        win_nrows, win_slot, win_stride, xq, out, ldo),
+              wh_launched("k_xattn_seg<qproj>");
+        else
+          k_xattn_seg<T, 0, 8, float, false, 20><<<nwg_xs, 512, 0, st>>>(q, ldq, ck, cv, Tk, H, npair, nsp, win_row0,
+                                                                         win_nrows, win_slot, win_stride, xq, out, ldo),
+              wh_launched("k_xattn_seg<qproj>");
+      } else {
+        wh_set_launch_error("launch_cross_attn: fused query projection in an fp32 context");
+      }
+      return;
+    }
 #define XSF(QZ_, RR_, S_)                                                                                         \
   if (full)                                                                                                     \
     k_xattn_seg<T, QZ_, RR_, S_, true><<<nwg_xs, 512, 0, st>>>(q, ldq, ck, cv, Tk, H, npair, nsp, win_row0,       \

@@ -927,7 +927,10 @@ struct Ctx : public wh_ctx {
       // k_cross_attn (rows per window <= Gcap <= 8), otherwise projected directly
       XQPart xq;
       if (skinny) xq = step_xq(ancG);
-      if (skinny && xq_fused) {
+      if (skinny && xq_proj_active(ancG)) {
+        // round 6: no cross-q launch; k_xattn_seg projects the LayerNorm'd rows itself
+        xq.qx = xn_d; xq.qw = e.wqx; xq.bias = e.bqx;
+      } else if (skinny && xq_fused) {
         int ks = 0;
         TRY(partial(xn_d, n, e.wqx, R, n, n, &ks));
         if (cross_attn_q_slabs(ks)) {
@@ -1025,6 +1028,7 @@ struct Ctx : public wh_ctx {
   std::string step_kernels(int n_win, int group) const override {
     const bool p1 = p1_active(n_win * group, n_win), h = sizeof(T) == 2;
     return std::string("proj=") + (p1 ? "k_proj1" : "k_proj") + ",xattn=k_xattn_seg" +
+           (!p1 && xq_proj_active(group) ? "<qproj>" : "") +
            ",self_attn=" +
            (p1 ? "k_self_attn"
                : h && group >= 2 && self_attn_grp_mode() ? "k_self_attn_grp"
@@ -1425,6 +1429,19 @@ struct Ctx : public wh_ctx {
     const char* e = tune_env("WHISPER_HIP_XQ");
     return !(e && e[0] == '0');
   }();
+  // round 6: the step's cross-attention query projected inside k_xattn_seg (no cross-q
+  // k_proj launch) wherever xattn_fused_q serves the shape; WHISPER_HIP_XQP=0 keeps the
+  // split-K projection + slabs (A/B switch)
+  static bool xq_proj_on() {
+    static const bool on = [] {
+      const char* e = tune_env("WHISPER_HIP_XQP");
+      return !(e && e[0] == '0');
+    }();
+    return on;
+  }
+  bool xq_proj_active(int rows_per_window) const {
+    return xq_proj_on() && xattn_fused_q(ns, rows_per_window, (int)sizeof(T));
+  }
 
   // WHISPER_HIP_EAGER=1 launches the step kernels directly instead of replaying the
   // captured graph (same kernels; used under profilers that do not follow graphs)
@@ -1515,11 +1532,29 @@ struct Ctx : public wh_ctx {
   // anc layout), optional raw cross-QK of the alignment heads into d_aqk [na][n][1500];
   // on return xn_d holds the final LayerNorm of every row.  The host vectors are kept
   // alive in `keep` until the caller synchronises.
+  // A first pass writes beam slot 0's self-KV rows of its slot: refused on a slot that the
+  // live device-loop batch is still decoding (its done flag unset), which it would corrupt.
+  // Slots outside the batch, finished windows and the per-step ABI's batch are allowed.
+  int check_slot_idle(int slot) {
+    if (cur_nwin < 1 || step_api) return 0;
+    for (int w = 0; w < cur_nwin; ++w)
+      if (win_slots[w] == slot) {
+        int d = 0;
+        HIPCHK(hipMemcpyAsync(&d, S.done + w, 4, hipMemcpyDeviceToHost, st));
+        HIPCHK(hipStreamSynchronize(st));
+        if (!d)
+          return fail(-15, "slot " + std::to_string(slot) + " is still decoding (window " + std::to_string(w) +
+                               " of the current batch): a first pass would overwrite its self-KV rows");
+      }
+    return 0;
+  }
+
   int first_pass(int slot, const int* tokens, int n, const int* ah, int na, float* d_aqk,
                  std::vector<std::vector<int>>& keep) {
     if (!finalized) return fail(-9, "weights not finalized");
-    rows_dirty = true;  // the first pass runs its rows through x_d / row_pos
     if (slot < 0 || slot >= Wcap || n < 1 || n > CTX) return fail(-15, "bad slot or token count");
+    TRY(check_slot_idle(slot));
+    rows_dirty = true;  // the first pass runs its rows through x_d / row_pos
     for (int i = 0; i < n; ++i)
       if (tokens[i] < 0 || tokens[i] >= V) return fail(-15, "token out of vocabulary");
     keep.assign(9, {});
@@ -1584,6 +1619,7 @@ struct Ctx : public wh_ctx {
       if (n > CTX) return fail(-15, "align: more than 448 tokens");
       if (F < 1 || F > 1500) return fail(-15, "align: num_frames out of range");
       if (slots[w] < 0 || slots[w] >= Wcap) return fail(-15, "align: bad slot");
+      TRY(check_slot_idle(slots[w]));
       const int N = Tt + 1;
       tok_off[w + 1] = tok_off[w] + n;
       prob_off[w + 1] = prob_off[w] + Tt;
@@ -1637,6 +1673,9 @@ struct Ctx : public wh_ctx {
       }
       for (int q = 0; q < R; ++q)
         if (rt[q] < 0 || rt[q] >= V) return fail(-15, "align: token out of vocabulary");
+      // set before the first upload into row_pos / x_d (as first_pass does): a failing copy
+      // below must still make the next decode_steps re-embed its rows
+      rows_dirty = true;  // this first pass runs its rows through x_d / row_pos
       HIPCHK(hipMemcpyAsync(row_tok, rt.data(), R * 4, hipMemcpyHostToDevice, st));
       HIPCHK(hipMemcpyAsync(row_pos, rp.data(), R * 4, hipMemcpyHostToDevice, st));
       HIPCHK(hipMemcpyAsync(row_win, rw.data(), R * 4, hipMemcpyHostToDevice, st));
@@ -1644,7 +1683,6 @@ struct Ctx : public wh_ctx {
       HIPCHK(hipMemcpyAsync(win_row0, wr0.data(), nw * 4, hipMemcpyHostToDevice, st));
       HIPCHK(hipMemcpyAsync(win_nrows, wnr.data(), nw * 4, hipMemcpyHostToDevice, st));
       HIPCHK(hipMemcpyAsync(win_slot, wsl.data(), nw * 4, hipMemcpyHostToDevice, st));
-      rows_dirty = true;  // this first pass runs its rows through x_d / row_pos
       launch_embed<T>(E, Pdec, ns, row_tok, row_pos, nullptr, nullptr, 1, HCTX, CTX - 1, x_d, R, st);
       TRY(dec_layers(R, row_win, row_slot, row_pos, 1, nw, win_row0, win_nrows, win_slot, d_qk, qk_map, R, false,
                      fp_anc));
@@ -1776,7 +1814,10 @@ struct Ctx : public wh_ctx {
           } else {
             const T* ck = ckv + (size_t)(2 * l) * Wcap * TKP * n;
             const T* cv = ckv + (size_t)(2 * l + 1) * Wcap * TKP * n;
-            const XQPart xq = step_xq(cur_G);  // the step's kernel (k_xattn_seg), query from q_d
+            XQPart xq = step_xq(cur_G);  // the step's kernel (k_xattn_seg), query from q_d
+            if (xq_proj_active(cur_G)) {  // or projected in the kernel from xn_d (as the step does)
+              xq.qx = xn_d; xq.qw = e.wqx; xq.bias = e.bqx;
+            }
             launch_cross_attn<T>(q_d, n, ck, cv, 1500, nh, NSPLIT, cur_nwin, st_win_row0, st_win_nrows, st_win_slot,
                                  (int64_t)TKP * n, po, pm, pl, att_d, n, R, nullptr, nullptr, 0, st, xq);
             ++launches;

@@ -144,10 +144,23 @@ class DeviceAudio:
         self.n_samples = n_samples
 
 
+def max_windows_limit(dims: dict, dtype: str, max_group: int) -> int:
+    """Largest max_windows a context can hold: the self-attention kernels address one
+    layer's self-K / V cache ([windows][max_group][n_text_ctx][n]) with 32-bit byte offsets,
+    so it must stay under 2 GiB (wh_runtime.hip init refuses larger caches)."""
+    elem = 2 if dtype == "fp16" else 4
+    per_window = int(max_group) * int(dims["n_text_ctx"]) * int(dims["n_text_state"]) * elem
+    return max(0, ((1 << 31) - 4096 - 1) // per_window)
+
+
 class HipContext:
     """One libwhisper_hip context = one model on one GPU (per process)."""
 
     def __init__(self, dims: dict, device: int = 0, dtype: str = "fp16", max_windows: int = 8, max_group: int = 5):
+        lim = max_windows_limit(dims, dtype, max_group)
+        if max_windows > lim:
+            raise ValueError(f"max_windows={max_windows} with max_group={max_group} in {dtype}: one layer's self-KV cache "
+                             f"would exceed 2 GiB (32-bit offsets in the self-attention kernels); at most {lim} windows")
         self.lib = load_library()
         self.dims = dict(dims)
         self.dtype = dtype
@@ -171,8 +184,13 @@ class HipContext:
         """Release the context; raises HipBackendError if a HIP release failed (wh_destroy
         reports it instead of leaving the error pending for the next context)."""
         if getattr(self, "h", None):
-            h, self.h = self.h, None
-            self._check(self.lib.wh_destroy(h), "wh_destroy")
+            rc = self.lib.wh_destroy(self.h)
+            # -1: refused (other contexts still read this one's weights), the context is
+            # intact: keep the handle so close() can be retried once they are gone.  Any
+            # other code: the context is released (a non-zero code reports a failed release)
+            if rc != -1:
+                self.h = None
+            self._check(rc, "wh_destroy")
 
     def __del__(self):
         try:
