@@ -1088,10 +1088,13 @@ static bool select_rows(float* logits, int ldl, const DecState& s, const DecOpts
   }();
   const int rows = nwin * s.G;
   const bool merge = em && fold_merge && s.lpw_cnt && s.G <= MG_MAXG;
-  // the window-level arrival (k_logit_part<..., WIN>) unless WHISPER_HIP_LP_WIN=0 (tuning)
+  // the window-level arrival (k_logit_part<..., WIN>): tuning build only, WHISPER_HIP_LP_WIN=1.
+  // Measured not faster (profiles/r06/ab_selection_window_arrival.txt: 100 rows 51.5 vs
+  // 51.2 us, one turbo window 27.2 vs 28.5-28.9 us: the last slice's workgroup combining
+  // every row after the last arrival costs what the row-then-window hand-off saved)
   static const bool win_on = [] {
     const char* e = tune_env("WHISPER_HIP_LP_WIN");
-    return !(e && e[0] == '0');
+    return e && e[0] == '1';
   }();
   auto lp_win_fits = [&](int ns) {
     return win_on && (size_t)s.G * ns * LP_REC * 4 <= sizeof(MergeLds::oh) + sizeof(MergeLds::oa);

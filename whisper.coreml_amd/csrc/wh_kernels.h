@@ -50,6 +50,11 @@ struct XQPart {
   // with qx the LayerNorm'd rows [rows][n] and qw = W_q [n][n] (T); q / part unused
   const void* qx = nullptr;
   const void* qw = nullptr;
+  // the single-window step (k_proj1 layers): qx is the fp32 residual rows and the kernel
+  // computes their LayerNorm (ln_g, ln_b, ln_eps) itself — no cross-q k_proj1 launch
+  const float* ln_g = nullptr;
+  const float* ln_b = nullptr;
+  float ln_eps = 1e-5f;
 };
 // the shapes the in-kernel query projection serves: fp16, n = 1280 (large-v3, turbo), <= 8
 // rows per window; the choice depends on the model and the beam group only, never on the

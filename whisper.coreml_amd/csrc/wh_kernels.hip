@@ -1559,21 +1559,42 @@ __device__ unsigned long long g_xs_trace[256][XS_MARKS];
 // (MFMA accumulation in k-step order; the two halves meet in LDS in that order), the
 // same arithmetic whichever workgroup, grid form or batch computes it (batch invariance).
 // The 8 waves are (16-column tile c of the head's 64, K half kh); a pair's window rows
-// (<= RR) are staged in LDS (rows past the window read 0 through the buffer limit: their
-// queries are never emitted), the wave's 16 x n / 2 slice of W_q (QK fragments) is loaded
-// once per head, and the first tile's K / V leave before the wait (clamped: no branch).
-// X is staged in the tile partials' LDS (dead until the first tile) and the halves' sum
-// goes through it too.  Reference: decoder.py:73-91 (cross-attention query), :42 (scale).
+// (<= RR) are staged in LDS (rows past the window are never emitted), the wave's
+// 16 x n / 2 slice of W_q (QK fragments) is loaded once per head.  X, the K-half sums and
+// the biases live in the tile partials' LDS (dead until the first tile).  Reference:
+// decoder.py:73-91 (cross-attention query), :42 (the 0.125 query scale, folded in W_q).
+//
+// Load order variants (QV; the arithmetic is the same in all three):
+//  0: X (registers), bias, W_q, then the first tile's K / V; the second tile is loaded by the
+//     tile loop.  Traced at 20 windows (profiles/r06/xattn_trace_qv.txt): X staged at 8.8 us
+//     — the X and bias requests queue behind every CU's W_q and first-tile K / V (63 MB asked
+//     for at once), so the query was staged at 10.5 us against 4.4 with the slabs.
+//  1: X and biases by LDS-DMA (no VGPRs), the first two tiles' K / V with W_q.  hipcc puts a
+//     vmcnt(0) ahead of the first LDS read after an LDS-DMA (it cannot tell the DMA's slot
+//     in the count), so the projection waits for both tiles as well.
+//  2: X and bias (registers) and W_q first; the two tiles' K / V are issued only once X is
+//     staged, so the few KB the projection waits on are not queued behind 25 MB of K / V;
+//     the tiles then stream while W_q lands and the projection runs.
+//  3: variant 2 for the single-window step (k_proj1 layers, no k_resid_ln): X is the fp32
+//     residual rows and each workgroup computes their LayerNorm (k_proj1's arithmetic: one
+//     wave per row, two register passes) into the staged fp16 rows; the grid gives every
+//     workgroup tiles of ONE pair (launch_cross_attn).
 constexpr int XS_QF = 3;
-template <typename T, int QK, int RR, typename PairWH, typename LoadKV>
+template <typename T, int QK, int RR, int QV, typename PairWH, typename LoadKV>
 WH_DEV void xq_project(const XQPart& xq, int pa, int plast, int cnt, const int* __restrict__ win_row0,
                        const int* __restrict__ win_nrows, PairWH pair_wh, LoadKV load_kv, Frag<T> (&kA)[4][2],
-                       Frag<T> (&vA)[4][2], char* xst, T (*qs)[16][72], int* s_wnr, int* s_wr0) {
+                       Frag<T> (&vA)[4][2], Frag<T> (&kB)[4][2], Frag<T> (&vB)[4][2], char* xst, T (*qs)[16][72],
+                       int* s_wnr, int* s_wr0) {
   static_assert(sizeof(T) == 2, "fused query projection: fp16 contexts");
   constexpr int N = QK * 64;                           // model width = K
   constexpr int CPR = N * (int)sizeof(T) / 16;         // 16-B chunks per row
-  constexpr int XROWB = N * (int)sizeof(T) + 16;       // padded LDS row (bytes)
+  constexpr bool DMA = QV == 1;                        // X / bias by LDS-DMA
+  constexpr int XROWB = DMA ? N * (int)sizeof(T) : N * (int)sizeof(T) + 16;  // LDS row (bytes)
   constexpr int XPT = (RR * CPR + 511) / 512;          // chunks per thread per pair
+  static_assert(!DMA || (RR * CPR) % 64 == 0, "whole 1 KB LDS-DMA blocks per pair");
+  static_assert(!DMA || CPR % 8 == 0, "the row swizzle stays inside the row");
+  // LDS (byte offsets in xst): X rows, the K-half sums [2][XS_QF][4][64] float4, the biases
+  constexpr int RED_OFF = XS_QF * RR * XROWB, BIAS_OFF = RED_OFF + 2 * XS_QF * 4 * 64 * 16;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = lane & 15, g = lane >> 4;
   const int c = wave & 3, kh = wave >> 2;
   const int np = plast - pa + 1;
@@ -1588,23 +1609,64 @@ WH_DEV void xq_project(const XQPart& xq, int pa, int plast, int cnt, const int* 
     q_nr[j] = win_nrows[wj];
     q_r0[j] = win_row0[wj];
   }
-  // 1. each pair's window rows -> registers (unconditional loads; the buffer limit is the
-  // window's rows, 0 for pairs past the range)
-  float4_t xv[XS_QF][XPT];
+  // 1. each pair's window rows and head biases
+  constexpr bool LN = QV == 3;
+  constexpr int CPL = N / 256;  // (LN) float4 chunks of a fp32 row per lane
+  float4_t xv[DMA ? 1 : XS_QF][DMA ? 1 : XPT];
+  float bv[DMA ? 1 : XS_QF];
+  float4_t lx[LN ? CPL : 1], lg[LN ? CPL : 1], lb[LN ? CPL : 1];
+  if constexpr (LN) {
+    // wave w: row min(w, nr - 1) of the range's one pair (every LDS row a real row)
+    const float* xr = reinterpret_cast<const float*>(xq.qx) + (int64_t)(q_r0[0] + min(wave, q_nr[0] - 1)) * N;
 #pragma unroll
-  for (int j = 0; j < XS_QF; ++j) {
-    const auto rs = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<T*>(reinterpret_cast<const T*>(xq.qx)) + (int64_t)q_r0[j] * N, 0, j < np ? q_nr[j] * N * (int)sizeof(T) : 0,
-        0x00020000);
-#pragma unroll
-    for (int i = 0; i < XPT; ++i) {
-      const int ch = tid + 512 * i, off = (ch / CPR) * (N * (int)sizeof(T)) + (ch % CPR) * 16;
-      xv[j][i] = __builtin_bit_cast(float4_t, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0));
+    for (int i = 0; i < CPL; ++i) {
+      lx[i] = load4f(xr + 4 * (lane + 64 * i));
+      lg[i] = load4f(xq.ln_g + 4 * (lane + 64 * i));
+      lb[i] = load4f(xq.ln_b + 4 * (lane + 64 * i));
     }
-  }
-  float4_t bq[XS_QF];
+    bv[0] = xq.bias[q_h[0] * 64 + lane];
+  } else if constexpr (DMA) {
+    // LDS chunk q of pair j's block holds row q / CPR, chunk (q % CPR) ^ (row & 7) (rows past
+    // the window repeat its last row, pairs past the range the last pair: never read)
+    constexpr int NBLK = RR * CPR / 64, BPW = (NBLK + 7) / 8;  // 1 KB blocks per pair, per wave
 #pragma unroll
-  for (int j = 0; j < XS_QF; ++j) bq[j] = load4f(xq.bias + q_h[j] * 64 + c * 16 + 4 * g);
+    for (int j = 0; j < XS_QF; ++j) {
+      const int jj = min(j, np - 1);
+      const char* src = reinterpret_cast<const char*>(xq.qx) + (int64_t)q_r0[jj] * (N * (int)sizeof(T));
+#pragma unroll
+      for (int t = 0; t < BPW; ++t) {
+        const int blk = min(wave + 8 * t, NBLK - 1), q = blk * 64 + lane, row = q / CPR, cs = q - row * CPR;
+        const char* sp = src + min(row, q_nr[jj] - 1) * (N * (int)sizeof(T)) + ((cs ^ (row & 7)) * 16);
+        __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)(sp),
+                                         (__attribute__((address_space(3))) void*)(xst + (j * RR * CPR + blk * 64) * 16),
+                                         16, 0, 0);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < XS_QF; ++j)
+      if (lane < 16)  // 16 lanes x 16 B: the head's 64 fp32 biases
+        __builtin_amdgcn_global_load_lds(
+            (__attribute__((address_space(1))) void*)(xq.bias + q_h[min(j, np - 1)] * 64 + 4 * lane),
+            (__attribute__((address_space(3))) void*)(xst + BIAS_OFF + j * 256), 16, 0, 0);
+  } else {
+    // unconditional buffer loads: the buffer limit is the window's rows (0 past it and for
+    // pairs past the range); the biases by wave 0, one float per lane and pair
+    static_assert(N % 256 == 0 || !LN, "LN rows: whole float4 chunks per lane");
+#pragma unroll
+    for (int j = 0; j < XS_QF; ++j) {
+      const auto rs = __builtin_amdgcn_make_buffer_rsrc(
+          const_cast<T*>(reinterpret_cast<const T*>(xq.qx)) + (int64_t)q_r0[j] * N, 0, j < np ? q_nr[j] * N * (int)sizeof(T) : 0,
+          0x00020000);
+#pragma unroll
+      for (int i = 0; i < XPT; ++i) {
+        const int ch = tid + 512 * i, off = (ch / CPR) * (N * (int)sizeof(T)) + (ch % CPR) * 16;
+        xv[j][i] = __builtin_bit_cast(float4_t, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0));
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < XS_QF; ++j) bv[j] = xq.bias[q_h[min(j, np - 1)] * 64 + lane];
+  }
+  __builtin_amdgcn_sched_barrier(0);
   // 2. the wave's W_q fragments for the first pair's head: rows h*64 + 16c + r, K half kh
   Frag<T> wf[QK];
   auto load_w = [&](int h) {
@@ -1613,18 +1675,57 @@ WH_DEV void xq_project(const XQPart& xq, int pa, int plast, int cnt, const int* 
     for (int s = 0; s < QK; ++s) frag_load_stream(wf[s], wp + s * 32);
   };
   load_w(q_h[0]);
-  // 3. the first tile's K / V
-  load_kv(min(wave, cnt - 1), kA, vA);
   __builtin_amdgcn_sched_barrier(0);
-  // 4. X -> LDS (waits for the X loads alone: they were issued first)
+  // 3. (QV 0 / 1) the first tile's K / V, (1) the second's too
+  if constexpr (QV <= 1) {
+    load_kv(min(wave, cnt - 1), kA, vA);
+    if constexpr (QV == 1) load_kv(min(wave + 8, cnt - 1), kB, vB);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  // 4. X (and the biases) -> LDS: waits for them alone (issued first; vmcnt retires in order)
+  if constexpr (LN) {
+    // LayerNorm of the wave's row (biased variance, two passes in registers: k_proj1's
+    // prologue arithmetic), stored as the fp16 row
+    float sm = 0.f;
 #pragma unroll
-  for (int j = 0; j < XS_QF; ++j)
+    for (int i = 0; i < CPL; ++i) sm += lx[i][0] + lx[i][1] + lx[i][2] + lx[i][3];
+    const float mean = wave_sum(sm) / (float)N;
+    float qv2 = 0.f;
 #pragma unroll
-    for (int i = 0; i < XPT; ++i) {
-      const int ch = tid + 512 * i;
-      if (ch < RR * CPR)
-        *reinterpret_cast<float4_t*>(xst + (j * RR + ch / CPR) * XROWB + (ch % CPR) * 16) = xv[j][i];
+    for (int i = 0; i < CPL; ++i)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float d = lx[i][e] - mean;
+        qv2 += d * d;
+      }
+    const float rstd = rsqrtf(wave_sum(qv2) / (float)N + xq.ln_eps);
+    if (wave < RR) {
+#pragma unroll
+      for (int i = 0; i < CPL; ++i) {
+        const float4_t v = lx[i];
+        store4(reinterpret_cast<T*>(xst + wave * XROWB) + 4 * (lane + 64 * i), (v[0] - mean) * rstd * lg[i][0] + lb[i][0],
+               (v[1] - mean) * rstd * lg[i][1] + lb[i][1], (v[2] - mean) * rstd * lg[i][2] + lb[i][2],
+               (v[3] - mean) * rstd * lg[i][3] + lb[i][3]);
+      }
     }
+    if (wave == 0) reinterpret_cast<float*>(xst + BIAS_OFF)[lane] = bv[0];
+  } else if constexpr (DMA) {
+    static_assert(QK + 32 <= 63, "vmcnt range");
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(QK + 32) : "memory");
+  } else {
+#pragma unroll
+    for (int j = 0; j < XS_QF; ++j)
+#pragma unroll
+      for (int i = 0; i < XPT; ++i) {
+        const int ch = tid + 512 * i;
+        if (ch < RR * CPR)
+          *reinterpret_cast<float4_t*>(xst + (j * RR + ch / CPR) * XROWB + (ch % CPR) * 16) = xv[j][i];
+      }
+    if (wave == 0) {
+#pragma unroll
+      for (int j = 0; j < XS_QF; ++j) reinterpret_cast<float*>(xst + BIAS_OFF)[j * 64 + lane] = bv[j];
+    }
+  }
   if (tid == 0) {  // the merge's window rows (LDS, behind the barriers below)
 #pragma unroll
     for (int j = 0; j < XS_QF; ++j) {
@@ -1634,44 +1735,47 @@ WH_DEV void xq_project(const XQPart& xq, int pa, int plast, int cnt, const int* 
   }
   wh_lds_barrier();
   XS_MARK(7);  // X staged
-  // 5. pair by pair: MFMAs in k-step order (W reloaded only where the head changes)
-  float4_t qa[XS_QF];
+  // 3'. (QV 2 / 3) the first two tiles' K / V leave now, behind the few KB the projection waited on
+  if constexpr (QV >= 2) {
+    load_kv(min(wave, cnt - 1), kA, vA);
+    load_kv(min(wave + 8, cnt - 1), kB, vB);
+  }
+  // 5. pair by pair: MFMAs in k-step order (W reloaded only where the head changes); each
+  // pair's K-half sum goes to LDS at once (no register per pair)
+  float4_t* red2 = reinterpret_cast<float4_t*>(xst + RED_OFF);  // [kh][pair][c][lane]
 #pragma unroll
   for (int j = 0; j < XS_QF; ++j) {
-    qa[j] = (float4_t){0.f, 0.f, 0.f, 0.f};
     if (j < np) {
       if (j > 0 && q_h[j] != q_h[j - 1]) load_w(q_h[j]);
-      const char* xl = xst + (j * RR + min(r, RR - 1)) * XROWB + (kh * QK * 32 + 8 * g) * (int)sizeof(T);
+      float4_t acc = (float4_t){0.f, 0.f, 0.f, 0.f};
+      const int rr = min(r, RR - 1);
+      const char* xl = xst + (j * RR + rr) * XROWB;
 #pragma unroll
       for (int s = 0; s < QK; ++s) {
         Frag<T> xf;
-        frag_load(xf, reinterpret_cast<const T*>(xl + s * 32 * (int)sizeof(T)));
-        mfma_step(qa[j], wf[s], xf);
+        const int ch = kh * QK * 4 + 4 * s + g;  // 16-B chunk of k = kh * N / 2 + 32 s + 8 g
+        frag_load(xf, reinterpret_cast<const T*>(xl + (DMA ? (ch ^ (rr & 7)) : ch) * 16));
+        mfma_step(acc, wf[s], xf);
       }
+      red2[((kh * XS_QF + j) * 4 + c) * 64 + lane] = acc;
     }
   }
   XS_MARK(8);  // this wave's (thread 0's) MFMAs done: its W_q fragments landed
   // 6. the K halves meet (half 0 + half 1, then the bias) -> qs[pair][row][64] (fp16)
-  wh_lds_barrier();  // every wave's X reads are done: the area is reused
-  float4_t* red = reinterpret_cast<float4_t*>(xst);  // [XS_QF][4][64]
-  if (kh == 1) {
-#pragma unroll
-    for (int j = 0; j < XS_QF; ++j)
-      if (j < np) red[(j * 4 + c) * 64 + lane] = qa[j];
-  }
   wh_lds_barrier();
   if (kh == 0) {
+    const float* bl = reinterpret_cast<const float*>(xst + BIAS_OFF);
 #pragma unroll
     for (int j = 0; j < XS_QF; ++j)
       if (j < np) {
-        float4_t v = qa[j] + red[(j * 4 + c) * 64 + lane];
-        v += bq[j];
+        float4_t v = red2[(j * 4 + c) * 64 + lane] + red2[((XS_QF + j) * 4 + c) * 64 + lane];
+        v += *reinterpret_cast<const float4_t*>(bl + j * 64 + c * 16 + 4 * g);
         store4(&qs[j][r][c * 16 + 4 * g], v[0], v[1], v[2], v[3]);
       }
   }
 }
 
-template <typename T, int QZ, int RR, typename S = float, bool FULL = false, int QK = 0>
+template <typename T, int QZ, int RR, typename S = float, bool FULL = false, int QK = 0, int QV = 0>
 __global__ __launch_bounds__(512, 1) void k_xattn_seg(const T* __restrict__ q, int ldq, const T* ck, const T* cvt, int Tk,
                                                      int H, int npair, int nsp, const int* __restrict__ win_row0,
                                                      const int* __restrict__ win_nrows,
@@ -1797,10 +1901,11 @@ __global__ __launch_bounds__(512, 1) void k_xattn_seg(const T* __restrict__ q, i
   // profiles/xattn_trace.py: query staged at 5.3 us of a 34 us launch at 20 windows)
   constexpr int NQP = XS_QP / 2;
   if constexpr (QF) {
-    static_assert(XS_QF * RR * (QK * 64 * sizeof(T) + 16) <= sizeof(seg_o), "X rows in the partials' LDS");
+    static_assert(XS_QF * RR * (QK * 64 * sizeof(T) + 16) + 2 * XS_QF * 4 * 64 * 16 + XS_QF * 256 <= sizeof(seg_o),
+                  "X rows, K-half sums and biases in the partials' LDS");
     static_assert(XS_QF * 4 * 64 * 16 <= sizeof(seg_o), "K-half sums in the partials' LDS");
-    xq_project<T, QK, RR>(xq, pa, plast, cnt, win_row0, win_nrows, pair_wh, load_kv, kA, vA,
-                          reinterpret_cast<char*>(&seg_o[0][0][0]), qs, s_wnr, s_wr0);
+    xq_project<T, QK, RR, QV>(xq, pa, plast, cnt, win_row0, win_nrows, pair_wh, load_kv, kA, vA, kB, vB,
+                              reinterpret_cast<char*>(&seg_o[0][0][0]), qs, s_wnr, s_wr0);
   } else {
   // FULL (the launcher: every workgroup holds >= 8 tiles, one per wave at least): the order
   // above; otherwise (few windows, <= 1 tile per wave) the first tile leaves first, as the
@@ -1870,7 +1975,23 @@ __global__ __launch_bounds__(512, 1) void k_xattn_seg(const T* __restrict__ q, i
   asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // LDS only
   XS_MARK(1);
 
-  if (wave < cnt) {
+  if (QF && QV >= 1 && wave < cnt) {
+    // (QV 1 / 2) kB / vB already hold tile wave + NW (clamped): the next tile is in flight on
+    // entry, so each iteration refills the buffer it has just computed
+    int i = wave;
+    for (; i + 2 * NW < cnt; i += 2 * NW) {
+      tile(kA, vA, i);
+      load_kv(i + 2 * NW, kA, vA);
+      tile(kB, vB, i + NW);
+      load_kv(min(i + 3 * NW, cnt - 1), kB, vB);
+    }
+    if (i + NW < cnt) {
+      tile(kA, vA, i);
+      tile(kB, vB, i + NW);
+    } else {
+      tile(kA, vA, i);
+    }
+  } else if (wave < cnt) {
     int i = wave;
     // two tiles per iteration, the next one always in flight (unconditional loads)
     for (; i + 2 * NW < cnt; i += 2 * NW) {
@@ -2013,14 +2134,37 @@ void launch_cross_attn(const T* q, int ldq, const T* ck, const T* cv, int Tk, in
           wh_set_launch_error("launch_cross_attn: fused query projection outside its shapes");
           return;
         }
-        if (full)
-          k_xattn_seg<T, 0, 8, float, true, 20><<<nwg_xs, 512, 0, st>>>(q, ldq, ck, cv, Tk, H, npair, nsp, win_row0,
-                                                                        win_nrows, win_slot, win_stride, xq, out, ldo),
-              wh_launched("k_xattn_seg<qproj>");
-        else
-          k_xattn_seg<T, 0, 8, float, false, 20><<<nwg_xs, 512, 0, st>>>(q, ldq, ck, cv, Tk, H, npair, nsp, win_row0,
-                                                                         win_nrows, win_slot, win_stride, xq, out, ldo),
-              wh_launched("k_xattn_seg<qproj>");
+        if (xq.ln_g) {
+          // the single-window step: fp32 rows + LayerNorm in the kernel; every workgroup holds
+          // 2 tiles of ONE pair (nsp even): 12 workgroups per pair, merged through records
+          if (nwin != 1 || !xq.ln_b || nsp % 2) {
+            wh_set_launch_error("launch_cross_attn: in-kernel LayerNorm query is the single-window form");
+            return;
+          }
+          k_xattn_seg<T, 0, 8, float, false, 20, 3><<<npair * nsp / 2, 512, 0, st>>>(
+              q, ldq, ck, cv, Tk, H, npair, nsp, win_row0, win_nrows, win_slot, win_stride, xq, out, ldo),
+              wh_launched("k_xattn_seg<qproj,ln>");
+          return;
+        }
+        // load-order variant (xq_project): 2 unless the tuning build's WHISPER_HIP_XQV says 0 / 1
+        static const int qv = [] {
+          const char* e = tune_env("WHISPER_HIP_XQV");
+          return e ? atoi(e) : 2;
+        }();
+#define XQF(FULL_, QV_)                                                                                            \
+  k_xattn_seg<T, 0, 8, float, FULL_, 20, QV_><<<nwg_xs, 512, 0, st>>>(q, ldq, ck, cv, Tk, H, npair, nsp, win_row0, \
+                                                                      win_nrows, win_slot, win_stride, xq, out, ldo), \
+      wh_launched("k_xattn_seg<qproj>")
+        if (full) {
+          if (qv == 2) XQF(true, 2);
+          else if (qv == 1) XQF(true, 1);
+          else XQF(true, 0);
+        } else {
+          if (qv == 2) XQF(false, 2);
+          else if (qv == 1) XQF(false, 1);
+          else XQF(false, 0);
+        }
+#undef XQF
       } else {
         wh_set_launch_error("launch_cross_attn: fused query projection in an fp32 context");
       }

@@ -1028,7 +1028,7 @@ struct Ctx : public wh_ctx {
   std::string step_kernels(int n_win, int group) const override {
     const bool p1 = p1_active(n_win * group, n_win), h = sizeof(T) == 2;
     return std::string("proj=") + (p1 ? "k_proj1" : "k_proj") + ",xattn=k_xattn_seg" +
-           (!p1 && xq_proj_active(group) ? "<qproj>" : "") +
+           (!p1 && xq_proj_active(group) ? "<qproj>" : p1 && xq_proj1_active(group) ? "<qproj,ln>" : "") +
            ",self_attn=" +
            (p1 ? "k_self_attn"
                : h && group >= 2 && self_attn_grp_mode() ? "k_self_attn_grp"
@@ -1075,13 +1075,19 @@ struct Ctx : public wh_ctx {
       launch_self_attn<T>(q_d, n, kc[l], vc[l], rw, rs, rp, A, ancG, Gcap, nh, CTX, att_d, n, R, st);
       TRY(resid(att_d, n, e.wo, e.bo, false));  // deferring it measured +1.0 us on cross-q, -0.2 here
       // cross-attention block
-      g = GemmArgs();
-      g.W = e.wqx; g.bias = e.bqx; g.M = R; g.N = n; g.K = n;
-      ln_in(g, e.lnx_g, e.lnx_b);
-      g.out = q_d; g.ldo = n;
-      TRY(p1(g, EPI_STORE, true));
-      ln_done();
-      const XQPart xq = step_xq(ancG);
+      XQPart xq = step_xq(ancG);
+      if (xq_proj1_active(ancG) && !pend) {
+        // round 6: no cross-q k_proj1 launch; the cross-attention normalises the window's
+        // fp32 rows and projects its query itself
+        xq.qx = xc; xq.qw = e.wqx; xq.bias = e.bqx; xq.ln_g = e.lnx_g; xq.ln_b = e.lnx_b; xq.ln_eps = 1e-5f;
+      } else {
+        g = GemmArgs();
+        g.W = e.wqx; g.bias = e.bqx; g.M = R; g.N = n; g.K = n;
+        ln_in(g, e.lnx_g, e.lnx_b);
+        g.out = q_d; g.ldo = n;
+        TRY(p1(g, EPI_STORE, true));
+        ln_done();
+      }
       const T* ck = ckv + (size_t)(2 * l) * Wcap * TKP * n;
       const T* cv = ckv + (size_t)(2 * l + 1) * Wcap * TKP * n;
       launch_cross_attn<T>(q_d, n, ck, cv, 1500, nh, NSPLIT, nwin, wr0, wnr, wsl, (int64_t)TKP * n, po, pm, pl, att_d,
@@ -1442,6 +1448,16 @@ struct Ctx : public wh_ctx {
   bool xq_proj_active(int rows_per_window) const {
     return xq_proj_on() && xattn_fused_q(ns, rows_per_window, (int)sizeof(T));
   }
+  // and in the single-window step (k_proj1 layers: the LayerNorm too); WHISPER_HIP_XQP1=0
+  // keeps the cross-q k_proj1 launch (A/B switch)
+  static bool xq_proj1_on() {
+    static const bool on = [] {
+      const char* e = tune_env("WHISPER_HIP_XQP1");
+      return !(e && e[0] == '0');
+    }();
+    return on;
+  }
+  bool xq_proj1_active(int rows_per_window) const { return xq_proj1_on() && xq_proj_active(rows_per_window); }
 
   // WHISPER_HIP_EAGER=1 launches the step kernels directly instead of replaying the
   // captured graph (same kernels; used under profilers that do not follow graphs)
@@ -1815,8 +1831,15 @@ struct Ctx : public wh_ctx {
             const T* ck = ckv + (size_t)(2 * l) * Wcap * TKP * n;
             const T* cv = ckv + (size_t)(2 * l + 1) * Wcap * TKP * n;
             XQPart xq = step_xq(cur_G);  // the step's kernel (k_xattn_seg), query from q_d
-            if (xq_proj_active(cur_G)) {  // or projected in the kernel from xn_d (as the step does)
-              xq.qx = xn_d; xq.qw = e.wqx; xq.bias = e.bqx;
+            if (p1_active(R, cur_nwin) ? xq_proj1_active(cur_G) : xq_proj_active(cur_G)) {
+              // or projected in the kernel (as the step does): from xn_d, or (single window)
+              // from the fp32 rows with the LayerNorm in the kernel
+              xq.qw = e.wqx; xq.bias = e.bqx;
+              if (p1_active(R, cur_nwin)) {
+                xq.qx = x_d; xq.ln_g = e.lnx_g; xq.ln_b = e.lnx_b;
+              } else {
+                xq.qx = xn_d;
+              }
             }
             launch_cross_attn<T>(q_d, n, ck, cv, 1500, nh, NSPLIT, cur_nwin, st_win_row0, st_win_nrows, st_win_slot,
                                  (int64_t)TKP * n, po, pm, pl, att_d, n, R, nullptr, nullptr, 0, st, xq);
