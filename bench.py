@@ -215,36 +215,41 @@ def decoder_step_bytes(dims, n_windows, beams, mean_ctx, elem=2):
     return weights + cross + selfkv
 
 
-def projection_bytes_per_launch(dims, rows, p1, elem=2):
-    """Algorithmic bytes of one decoder-step projection, averaged over the six per
-    decoder layer (qkv n->3n, out n->n, cross-q n->n, cross-out n->n, fc1 n->4n,
-    fc2 4n->n).  Split-K k_proj: weights N*K + activations rows*K (fp16) + fp32 result
-    rows*N.  k_proj1 (`p1`): weights N*K; the LayerNorm'd projections read the fp32
-    residual rows*K*4 + gamma/beta and write rows*N fp16; the residual ones read
-    rows*K fp16 and read + write the fp32 residual rows*N*4*2."""
+def projection_bytes_per_launch(dims, rows, p1, elem=2, fused_q=False):
+    """Algorithmic bytes of one decoder-step projection launch, averaged over the ones a
+    decoder layer runs: qkv n->3n, out n->n, cross-q n->n, cross-out n->n, fc1 n->4n,
+    fc2 4n->n — without the cross-q when the step projects it inside the cross-attention
+    (`fused_q`, round 6: five per layer).  Split-K k_proj: weights N*K + activations
+    rows*K (fp16) + the result rows*N (fp16 slabs in fp16 contexts, counted at 4 B: the
+    algorithmic output of the projection, not its slab format).  k_proj1 (`p1`): weights
+    N*K; the LayerNorm'd projections read the fp32 residual rows*K*4 + gamma/beta and write
+    rows*N fp16; the residual ones read rows*K fp16 and read + write the fp32 residual
+    rows*N*4*2."""
     n = dims["n_text_state"]
     if p1:
-        ln = [(3 * n, n), (n, n), (4 * n, n)]
+        ln = [(3 * n, n), (4 * n, n)] + ([] if fused_q else [(n, n)])
         res = [(n, n), (n, n), (n, 4 * n)]
         tot = sum(N * K * elem + rows * K * 4 + 2 * K * 4 + rows * N * elem for N, K in ln)
         tot += sum(N * K * elem + rows * K * elem + rows * N * 8 for N, K in res)
-        return tot // 6
-    shapes = [(3 * n, n), (n, n), (n, n), (n, n), (4 * n, n), (n, 4 * n)]
+        return tot // (len(ln) + len(res))
+    shapes = [(3 * n, n), (n, n), (n, n), (4 * n, n), (n, 4 * n)] + ([] if fused_q else [(n, n)])
     tot = sum(N * K * elem + rows * K * elem + rows * N * 4 for N, K in shapes)
     return tot // len(shapes)
 
 
-def cross_attn_bytes_per_launch(dims, n_windows, rows, elem=2):
-    """One layer's cross-attention: K and V of every window (2*1500*n) + q in / out."""
+def cross_attn_bytes_per_launch(dims, n_windows, rows, elem=2, fused_q=False):
+    """One layer's cross-attention: K and V of every window (2*1500*n) + q in / out; with
+    the query projected in the kernel (round 6) + the query weights n*n (the rows in are
+    the LayerNorm'd rows instead of q: the same rows*n)."""
     n = dims["n_text_state"]
-    return n_windows * 2 * 1500 * n * elem + 2 * rows * n * elem
+    return n_windows * 2 * 1500 * n * elem + 2 * rows * n * elem + (n * n * elem if fused_q else 0)
 
 
 def load_traffic(kernel):
     """HBM bytes per launch of `kernel` from the committed PMC pass
     (profiles/<round>/traffic.json, written by profiles/pmc_traffic.py: FETCH_SIZE x2
     + WRITE_SIZE per the gfx950 correction of MI355X_MICROARCH.md), or None."""
-    for rnd in ("r05", "r04", "r03", "r02", "r01"):
+    for rnd in ("r06", "r05", "r04", "r03", "r02", "r01"):
         path = os.path.join(REPO, "profiles", rnd, "traffic.json")
         try:
             with open(path) as f:
@@ -475,9 +480,10 @@ def main():
     gemv_b2b_ms = model.ctx.time_stage(2, 3)
     kern = model.ctx.step_kernels(n_win, args.beam)  # what the library runs for this batch
     p1 = kern["proj"] == "k_proj1"
-    gemv_bytes = projection_bytes_per_launch(dims, rows, p1)
+    fused_q = "<qproj" in kern["xattn"]  # the cross-q projected inside the cross-attention (round 6)
+    gemv_bytes = projection_bytes_per_launch(dims, rows, p1, fused_q=fused_q)
     xattn_ms = model.ctx.time_stage(3, 3)
-    xattn_bytes = cross_attn_bytes_per_launch(dims, n_win, rows)
+    xattn_bytes = cross_attn_bytes_per_launch(dims, n_win, rows, fused_q=fused_q)
     step_ms = model.ctx.time_stage(0, 20)
     step_bytes = decoder_step_bytes(dims, n_win, args.beam, mean_ctx)
 
@@ -509,7 +515,7 @@ def main():
     # k_xattn_seg) and at one window (k_proj1): other shapes report no traffic
     lv3 = args.model == "large-v3"
     traffic = load_traffic(kern["proj"]) if lv3 and (p1 or n_win == 20) else None
-    xattn_traffic = load_traffic(kern["xattn"]) if lv3 and n_win == 20 else None
+    xattn_traffic = load_traffic(kern["xattn"].split("<")[0]) if lv3 and n_win == 20 else None
     parallel = parallelism_label(world, file_seconds, args.balance)
     out = {
         "metric": "xRT (audio-s/s) large-v3 beam=5 @1/2/4/8 GPU; p50 per-token decode ms",
@@ -543,6 +549,7 @@ def main():
                      "frac": round(gbs(gemv_bytes, gemv_ms) / HBM_PEAK_GBS, 4),
                      "traffic": traffic, "bytes_per_launch": gemv_bytes, "ms_per_launch": round(gemv_ms, 5),
                      "timing": "HIP events around each launch inside eager decoder steps",
+                     "launches_per_layer": 5 if fused_q else 6,
                      "ms_per_launch_back_to_back": round(gemv_b2b_ms, 5),
                      "back_to_back_note": "time_stage 2: the six projections of each layer queued without their "
                                           "producers; on the k_proj1 path the non-deferred fc2 and the plain QKV "

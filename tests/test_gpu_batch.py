@@ -13,7 +13,9 @@ Bars (DESIGN.md §2 states them):
     selected): at every one of the 224 steps and every row,
         max |logit - ref| over the reference top-32  <=  TAU[dtype] * (top-32 range)
     with TAU = 2e-5 (fp32) and 1e-2 (fp16), at 1, 2, 3 and 20 windows (5 - 100 rows)
-    (measured worst cases, profiles/r02/gpu_tests.log: 7.6e-6 and 3.3e-3);
+    (measured worst cases, round 6 with fp16 split-K slabs and the in-kernel cross-attention
+    query: 9.3e-6 = 0.46 TAU and 3.9e-3 = 0.39 TAU, profiles/r06/fp16_margins.json; every
+    case's worst error, its step / row and top-1 agreement go to gpurun_out/margins.jsonl);
   * the reference's host loop (decoding.py:707-737, restated by the oracle) driving
     the per-step ABI through whisper.inference.HipInference: fp32 tokens exact.
 """

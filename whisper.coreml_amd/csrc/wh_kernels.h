@@ -13,9 +13,27 @@ void launch_layernorm(const float* x, T* y, const float* g, const float* b, int 
 // Split-K slabs of the decoder-step projections (k_proj EPI_PARTIAL) are fp32, or fp16 in
 // fp16 contexts (GemmArgs::slab_half): `part` then points at half_t
 // elements and slab_half is 1.  Strides count elements.
+// Round 6: an L2 prefetch ridden by a latency-bound launch for the NEXT launch of the same
+// stream.  Workgroup b of the carrying launch runs on XCD b % 8 (round-robin dispatch, as
+// xcd_remap assumes; speed only), and the workgroups on XCD x pull bytes [lo[x], hi[x]) x
+// unit of `base` into that XCD's L2 by LDS-DMA into a scratch block (no registers; the
+// carrying workgroup waits for them before it ends, so its LDS is never reallocated under
+// a transfer).  Used for the step cross-attention's W_q head slices (k_xattn_seg<qproj>):
+// read by 25 workgroups per XCD at once, they missed the L2 together and streamed from
+// memory at ~4 TB/s (profiles/r06/xattn_trace_xqv.txt).
+struct L2Prefetch {
+  const char* base = nullptr;
+  int64_t unit = 0;  // bytes per index (a W_q head slice: 64 rows x n)
+  int lo[8] = {0, 0, 0, 0, 0, 0, 0, 0}, hi[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+};
 template <typename T>
 void launch_resid_ln(float* x, const float* part, int nsplit, int64_t part_stride, const float* bias, T* y,
-                     const float* g, const float* b, int rows, int n, float eps, hipStream_t st, int slab_half = 0);
+                     const float* g, const float* b, int rows, int n, float eps, hipStream_t st, int slab_half = 0,
+                     const L2Prefetch* pf = nullptr);
+// the per-XCD head ranges of k_xattn_seg<qproj>'s workgroups for a batch (same grid and
+// xcd_remap as launch_cross_attn): pf->lo / hi in heads; false when the grid is too small
+// for the per-XCD runs (fewer than 16 workgroups)
+bool xattn_l2_ranges(int nwin, int H, int max_rows, L2Prefetch* pf);
 template <typename T>
 void launch_attn_enc(const T* qkv, int ld, int ns, int H, int Tlen, int nwin, int64_t wsi, const T* vt, int tkp, T* out,
                      int64_t wso, hipStream_t st);

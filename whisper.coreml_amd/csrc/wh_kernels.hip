@@ -67,12 +67,15 @@ void launch_layernorm(const float* x, T* y, const float* g, const float* b, int 
 // x[r] += bias + sum_s part[s][r] (fixed order: deterministic split-K reduction of the
 // residual GEMVs), then y = LayerNorm(x).  One 256-thread block per row; every load
 // of the row is issued before the first reduction (latency-bound at decode sizes).
-template <typename T, int NS, int MAXV = 2, typename S = float>
+// PF (round 6): the workgroup also carries its share of an L2Prefetch (wh_kernels.h) for the
+// next launch, issued after its own loads (they return first) and waited for at its end.
+template <typename T, int NS, int MAXV = 2, typename S = float, bool PF = false>
 __global__ __launch_bounds__(512) void k_resid_ln(float* __restrict__ x, const S* __restrict__ part, int nsplit,
                                                   int64_t part_stride, const float* __restrict__ bias,
                                                   T* __restrict__ y, const float* __restrict__ gamma,
-                                                  const float* __restrict__ beta, int n, float eps) {
+                                                  const float* __restrict__ beta, int n, float eps, L2Prefetch pf) {
   __shared__ float red[2][8];
+  __shared__ __attribute__((aligned(16))) char pf_sink[PF ? 1024 : 16];
   const int row = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, NT = blockDim.x, nwv = NT >> 6;
   CT_MARK(CT_RESID_LN, 0);
   float* xr = x + (int64_t)row * n;
@@ -100,6 +103,15 @@ __global__ __launch_bounds__(512) void k_resid_ln(float* __restrict__ x, const S
         if (sp < nsplit) a += (float4_t){(float)pp[sp][0], (float)pp[sp][1], (float)pp[sp][2], (float)pp[sp][3]};
       v[i] = a;
     }
+  }
+  if constexpr (PF) {
+    // this workgroup's share of its XCD's byte range, in 1 KB blocks dealt to its waves
+    const int xcd = blockIdx.x & 7, idx = blockIdx.x >> 3, m = ((int)gridDim.x - xcd + 7) >> 3;
+    const int64_t b0 = pf.lo[xcd] * pf.unit, nb = (pf.hi[xcd] - pf.lo[xcd]) * pf.unit / 1024;
+    const int64_t k0 = nb * idx / m, k1 = nb * (idx + 1) / m;
+    for (int64_t k = k0 + wv; k < k1; k += nwv)
+      __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)(pf.base + b0 + k * 1024 + lane * 16),
+                                       (__attribute__((address_space(3))) void*)(pf_sink), 16, 0, 0);
   }
   float s = 0.f;
 #pragma unroll
@@ -139,25 +151,34 @@ __global__ __launch_bounds__(512) void k_resid_ln(float* __restrict__ x, const S
       store4(yr + 4 * c, (v[i][0] - mean) * rstd * gm[i][0] + bt[i][0], (v[i][1] - mean) * rstd * gm[i][1] + bt[i][1],
              (v[i][2] - mean) * rstd * gm[i][2] + bt[i][2], (v[i][3] - mean) * rstd * gm[i][3] + bt[i][3]);
   }
+  if constexpr (PF) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS-DMA outlives the workgroup
   CT_END(CT_RESID_LN);
 }
 
+
 template <typename T>
 void launch_resid_ln(float* x, const float* part, int nsplit, int64_t part_stride, const float* bias, T* y,
-                     const float* g, const float* b, int rows, int n, float eps, hipStream_t st, int slab_half) {
+                     const float* g, const float* b, int rows, int n, float eps, hipStream_t st, int slab_half,
+                     const L2Prefetch* pf) {
   if (rows <= 0) return;
+  const L2Prefetch none;
   // one float4 per thread (n <= 2048; 1280: 5 waves); tuning builds WHISPER_HIP_RLN_256=1
   // for the round-3 form (256 threads, up to two float4 each)
   const char* e = tune_env("WHISPER_HIP_RLN_256");
   const int nt = (e && atoi(e) == 1) ? 256 : ((n >> 2) + 63) / 64 * 64;
   if (slab_half && nsplit > 0 && nt != 256) {  // fp16 slabs (fp16 contexts, k_proj)
     const half_t* ph = reinterpret_cast<const half_t*>(part);
-    if (nsplit <= 4) k_resid_ln<T, 4, 1, half_t><<<rows, nt, 0, st>>>(x, ph, nsplit, part_stride, bias, y, g, b, n, eps), wh_launched("k_resid_ln");
-    else k_resid_ln<T, 16, 1, half_t><<<rows, nt, 0, st>>>(x, ph, nsplit, part_stride, bias, y, g, b, n, eps), wh_launched("k_resid_ln");
+    if (pf && pf->base) {
+      if (nsplit <= 4) k_resid_ln<T, 4, 1, half_t, true><<<rows, nt, 0, st>>>(x, ph, nsplit, part_stride, bias, y, g, b, n, eps, *pf), wh_launched("k_resid_ln<pf>");
+      else k_resid_ln<T, 16, 1, half_t, true><<<rows, nt, 0, st>>>(x, ph, nsplit, part_stride, bias, y, g, b, n, eps, *pf), wh_launched("k_resid_ln<pf>");
+      return;
+    }
+    if (nsplit <= 4) k_resid_ln<T, 4, 1, half_t><<<rows, nt, 0, st>>>(x, ph, nsplit, part_stride, bias, y, g, b, n, eps, none), wh_launched("k_resid_ln");
+    else k_resid_ln<T, 16, 1, half_t><<<rows, nt, 0, st>>>(x, ph, nsplit, part_stride, bias, y, g, b, n, eps, none), wh_launched("k_resid_ln");
     return;
   }
 #define RLN(NS_, MV_) \
-  k_resid_ln<T, NS_, MV_><<<rows, nt, 0, st>>>(x, part, NS_ ? nsplit : 0, part_stride, bias, y, g, b, n, eps), wh_launched("k_resid_ln")
+  k_resid_ln<T, NS_, MV_><<<rows, nt, 0, st>>>(x, part, NS_ ? nsplit : 0, part_stride, bias, y, g, b, n, eps, none), wh_launched("k_resid_ln")
   if (nsplit <= 0) {
     if (nt == 256) RLN(0, 2); else RLN(0, 1);
   } else if (nsplit <= 4) {
@@ -1575,6 +1596,9 @@ __device__ unsigned long long g_xs_trace[256][XS_MARKS];
 //  2: X and bias (registers) and W_q first; the two tiles' K / V are issued only once X is
 //     staged, so the few KB the projection waits on are not queued behind 25 MB of K / V;
 //     the tiles then stream while W_q lands and the projection runs.
+//  4: variant 2 with the W_q fragments issued first, ahead of the window-row metadata round
+//     trip (their addresses need only the pair's head); 5: variant 4 with the two tiles'
+//     K / V issued only after the projection's MFMAs (nothing competes with W_q and X).
 //  3: variant 2 for the single-window step (k_proj1 layers, no k_resid_ln): X is the fp32
 //     residual rows and each workgroup computes their LayerNorm (k_proj1's arithmetic: one
 //     wave per row, two register passes) into the staged fp16 rows; the grid gives every
@@ -1598,16 +1622,29 @@ WH_DEV void xq_project(const XQPart& xq, int pa, int plast, int cnt, const int* 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = lane & 15, g = lane >> 4;
   const int c = wave & 3, kh = wave >> 2;
   const int np = plast - pa + 1;
-  // the pairs' heads and window rows: scalar loads, one round trip
-  int q_h[XS_QF], q_nr[XS_QF], q_r0[XS_QF];
+  // the pairs' heads (arithmetic only) and window rows (scalar loads, one round trip)
+  int q_h[XS_QF], q_w[XS_QF], q_nr[XS_QF], q_r0[XS_QF];
 #pragma unroll
   for (int j = 0; j < XS_QF; ++j) {
     const int pj = __builtin_amdgcn_readfirstlane(min(pa + j, plast));
-    int wj, hj;
-    pair_wh(pj, wj, hj);
-    q_h[j] = hj;
-    q_nr[j] = win_nrows[wj];
-    q_r0[j] = win_row0[wj];
+    pair_wh(pj, q_w[j], q_h[j]);
+  }
+  // QV 4 / 5: the wave's W_q fragments leave first, ahead of the metadata round trip
+  constexpr bool W_FIRST = QV >= 4;
+  Frag<T> wf[QK];
+  auto load_w = [&](int h) {
+    const T* wp = reinterpret_cast<const T*>(xq.qw) + (int64_t)(h * 64 + c * 16 + r) * N + kh * QK * 32 + 8 * g;
+#pragma unroll
+    for (int s = 0; s < QK; ++s) frag_load_stream(wf[s], wp + s * 32);
+  };
+  if constexpr (W_FIRST) {
+    load_w(q_h[0]);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+#pragma unroll
+  for (int j = 0; j < XS_QF; ++j) {
+    q_nr[j] = win_nrows[q_w[j]];
+    q_r0[j] = win_row0[q_w[j]];
   }
   // 1. each pair's window rows and head biases
   constexpr bool LN = QV == 3;
@@ -1668,14 +1705,10 @@ WH_DEV void xq_project(const XQPart& xq, int pa, int plast, int cnt, const int* 
   }
   __builtin_amdgcn_sched_barrier(0);
   // 2. the wave's W_q fragments for the first pair's head: rows h*64 + 16c + r, K half kh
-  Frag<T> wf[QK];
-  auto load_w = [&](int h) {
-    const T* wp = reinterpret_cast<const T*>(xq.qw) + (int64_t)(h * 64 + c * 16 + r) * N + kh * QK * 32 + 8 * g;
-#pragma unroll
-    for (int s = 0; s < QK; ++s) frag_load_stream(wf[s], wp + s * 32);
-  };
-  load_w(q_h[0]);
-  __builtin_amdgcn_sched_barrier(0);
+  if constexpr (!W_FIRST) {
+    load_w(q_h[0]);
+    __builtin_amdgcn_sched_barrier(0);
+  }
   // 3. (QV 0 / 1) the first tile's K / V, (1) the second's too
   if constexpr (QV <= 1) {
     load_kv(min(wave, cnt - 1), kA, vA);
@@ -1735,8 +1768,8 @@ WH_DEV void xq_project(const XQPart& xq, int pa, int plast, int cnt, const int* 
   }
   wh_lds_barrier();
   XS_MARK(7);  // X staged
-  // 3'. (QV 2 / 3) the first two tiles' K / V leave now, behind the few KB the projection waited on
-  if constexpr (QV >= 2) {
+  // 3'. (QV 2 - 4) the first two tiles' K / V leave now, behind the few KB the projection waited on
+  if constexpr (QV >= 2 && QV <= 4) {
     load_kv(min(wave, cnt - 1), kA, vA);
     load_kv(min(wave + 8, cnt - 1), kB, vB);
   }
@@ -1759,6 +1792,11 @@ WH_DEV void xq_project(const XQPart& xq, int pa, int plast, int cnt, const int* 
       }
       red2[((kh * XS_QF + j) * 4 + c) * 64 + lane] = acc;
     }
+  }
+  // 3''. (QV 5) the first two tiles' K / V only once the projection has its operands
+  if constexpr (QV == 5) {
+    load_kv(min(wave, cnt - 1), kA, vA);
+    load_kv(min(wave + 8, cnt - 1), kB, vB);
   }
   XS_MARK(8);  // this wave's (thread 0's) MFMAs done: its W_q fragments landed
   // 6. the K halves meet (half 0 + half 1, then the bias) -> qs[pair][row][64] (fp16)
@@ -2114,6 +2152,25 @@ int xattn_seg_grid(int npair, int nsp, int smax) {
   return nwg;
 }
 
+bool xattn_l2_ranges(int nwin, int H, int max_rows, L2Prefetch* pf) {
+  const int npair = nwin * H, nsp = XS_NSP, nseg = npair * nsp;
+  const int nwg = xattn_seg_grid(npair, nsp, max_rows <= 8 ? XsShape<8>::SMAX : XsShape<16>::SMAX);
+  if (nwg < 16) return false;
+  const int q = nwg / 8, r = nwg % 8;
+  for (int x = 0; x < 8; ++x) {
+    const int L0 = x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q, cnt = q + (x < r ? 1 : 0);
+    const unsigned s0 = (unsigned)L0 * (unsigned)nseg / (unsigned)nwg,
+                   s1 = (unsigned)(L0 + cnt) * (unsigned)nseg / (unsigned)nwg;  // range_split
+    if (cnt == 0 || s1 <= s0) {
+      pf->lo[x] = pf->hi[x] = 0;
+      continue;
+    }
+    pf->lo[x] = (int)(s0 / nsp) / nwin;             // head-major pairs: p = head * nwin + window
+    pf->hi[x] = (int)((s1 - 1) / nsp) / nwin + 1;
+  }
+  return true;
+}
+
 template <typename T>
 void launch_cross_attn(const T* q, int ldq, const T* ck, const T* cv, int Tk, int H, int nsplit, int nwin,
                        const int* win_row0, const int* win_nrows, const int* win_slot, int64_t win_stride, float* po,
@@ -2157,10 +2214,14 @@ void launch_cross_attn(const T* q, int ldq, const T* ck, const T* cv, int Tk, in
       wh_launched("k_xattn_seg<qproj>")
         if (full) {
           if (qv == 2) XQF(true, 2);
+          else if (qv == 4) XQF(true, 4);
+          else if (qv == 5) XQF(true, 5);
           else if (qv == 1) XQF(true, 1);
           else XQF(true, 0);
         } else {
           if (qv == 2) XQF(false, 2);
+          else if (qv == 4) XQF(false, 4);
+          else if (qv == 5) XQF(false, 5);
           else if (qv == 1) XQF(false, 1);
           else XQF(false, 0);
         }
@@ -2391,7 +2452,7 @@ void launch_mel_norm(float* mel, int64_t count, int64_t ld, int n_mels, const un
   template void launch_layernorm<T>(const float*, T*, const float*, const float*, int, int, float, const int*,     \
                                     hipStream_t);                                                                   \
   template void launch_resid_ln<T>(float*, const float*, int, int64_t, const float*, T*, const float*, const float*, \
-                                   int, int, float, hipStream_t, int);                                              \
+                                   int, int, float, hipStream_t, int, const L2Prefetch*);                           \
   template int launch_self_attn_qkv<T>(const float*, int, int64_t, const float*, int, T*, T*, const int*, const int*, \
                                         const int*, const int*, int, int, int, int, T*, int, int, hipStream_t, int); \
   template void launch_reduce_store<T>(const float*, int, int64_t, const float*, T*, int, int, int, int, hipStream_t, \

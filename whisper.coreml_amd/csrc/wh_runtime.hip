@@ -854,7 +854,9 @@ struct Ctx : public wh_ctx {
     return gemm(X, ldx, W, nullptr, R, N, K, EPI_PARTIAL, g);
   }
 
-  int resid(const T* X, int K, const T* W, const float* b, int R, const float* lg, const float* lb) {
+  // pf: an L2 prefetch for the next launch, carried by the split-K reduction (round 6)
+  int resid(const T* X, int K, const T* W, const float* b, int R, const float* lg, const float* lb,
+            const L2Prefetch* pf = nullptr) {
     const int n = ns;
     GemmArgs g;
     if (R > 128) {
@@ -864,9 +866,20 @@ struct Ctx : public wh_ctx {
     } else {
       int ks = 0;
       TRY(partial(X, K, W, R, n, K, &ks));
-      launch_resid_ln<T>(x_d, part, ks, (int64_t)R * n, b, xn_d, lg, lb, R, n, 1e-5f, st, slab_h);
+      launch_resid_ln<T>(x_d, part, ks, (int64_t)R * n, b, xn_d, lg, lb, R, n, 1e-5f, st, slab_h, pf);
     }
     return 0;
+  }
+  // the step cross-attention's W_q head slices into the L2 of the XCDs whose k_xattn_seg
+  // workgroups read them, by the k_resid_ln before it: tuning build only, WHISPER_HIP_XQ_PF=1.
+  // Measured slower (profiles/r06/ab_xq_l2_prefetch.txt: the k_resid_ln 1.4 us longer, the
+  // cross-attention not shorter — its query phase does not wait on L2 misses)
+  static bool xq_pf_on() {
+    static const bool on = [] {
+      const char* e = tune_env("WHISPER_HIP_XQ_PF");
+      return e && e[0] == '1';
+    }();
+    return on;
   }
 
   // out = act(xn W^T + b) for R rows (cross-attention query, MLP fc1): split-K
@@ -922,7 +935,13 @@ struct Ctx : public wh_ctx {
         TRY(gemm(xn_d, n, e.wqkv, e.bqkv, R, 3 * n, n, EPI_QKV_DEC, g));
         launch_self_attn<T>(q_d, n, kc[l], vc[l], rw, rs, rp, A, ancG, Gcap, nh, CTX, att_d, n, R, st);
       }
-      TRY(resid(att_d, n, e.wo, e.bo, R, e.lnx_g, e.lnx_b));
+      L2Prefetch pf;
+      const bool use_pf = skinny && xq_proj_active(ancG) && xq_pf_on() && xattn_l2_ranges(nwin, nh, ancG, &pf);
+      if (use_pf) {
+        pf.base = reinterpret_cast<const char*>(e.wqx);
+        pf.unit = (int64_t)64 * n * sizeof(T);
+      }
+      TRY(resid(att_d, n, e.wo, e.bo, R, e.lnx_g, e.lnx_b, use_pf ? &pf : nullptr));
       // cross-attention query: in step mode its split-K slabs are reduced inside
       // k_cross_attn (rows per window <= Gcap <= 8), otherwise projected directly
       XQPart xq;
@@ -999,6 +1018,7 @@ struct Ctx : public wh_ctx {
                        {nullptr, n, e.w1, e.b1, 4 * n, EPI_STORE_GELU, e.ln2_g, e.ln2_b, hm_d},
                        {hm_d, 4 * n, e.w2, e.b2, n, EPI_RESID, nullptr, nullptr, nullptr}};
       for (const Q& q : qs) {
+        if (q.W == e.wqx && xq_proj1_active(R)) continue;  // the step projects the cross-q in k_xattn_seg
         g = GemmArgs();
         g.W = q.W; g.bias = q.b; g.M = R; g.N = q.N; g.K = q.K;
         if (q.lg) {
@@ -1014,6 +1034,7 @@ struct Ctx : public wh_ctx {
         {xn_d, n, e.wqkv, 3 * n}, {att_d, n, e.wo, n}, {xn_d, n, e.wqx, n},
         {att_d, n, e.wox, n},     {xn_d, n, e.w1, 4 * n}, {hm_d, 4 * n, e.w2, n}};
     for (auto& p : ps) {
+      if (p.W == e.wqx && xq_proj_active(cur_G)) continue;  // the step projects the cross-q in k_xattn_seg
       int ks = 0;
       TRY(partial(p.X, p.K, p.W, R, p.N, p.K, &ks));
     }
@@ -1028,7 +1049,7 @@ struct Ctx : public wh_ctx {
   std::string step_kernels(int n_win, int group) const override {
     const bool p1 = p1_active(n_win * group, n_win), h = sizeof(T) == 2;
     return std::string("proj=") + (p1 ? "k_proj1" : "k_proj") + ",xattn=k_xattn_seg" +
-           (!p1 && xq_proj_active(group) ? "<qproj>" : p1 && xq_proj1_active(group) ? "<qproj,ln>" : "") +
+           (!p1 && xq_proj_active(group) ? "<qproj>" : p1 && xq_proj1_active(group) ? "<qproj+ln>" : "") +
            ",self_attn=" +
            (p1 ? "k_self_attn"
                : h && group >= 2 && self_attn_grp_mode() ? "k_self_attn_grp"
@@ -1448,12 +1469,15 @@ struct Ctx : public wh_ctx {
   bool xq_proj_active(int rows_per_window) const {
     return xq_proj_on() && xattn_fused_q(ns, rows_per_window, (int)sizeof(T));
   }
-  // and in the single-window step (k_proj1 layers: the LayerNorm too); WHISPER_HIP_XQP1=0
-  // keeps the cross-q k_proj1 launch (A/B switch)
+  // and in the single-window step (k_proj1 layers: the LayerNorm too): tuning build only,
+  // WHISPER_HIP_XQP1=1.  Measured slower (profiles/r06/ab_xqp1_single_window.txt): at one
+  // window 240 workgroups each ingest the 164 KB W_q slice of their head before any tile can
+  // run, and the cross-attention launch grows 6.1 -> 17.4 us against the 5-7 us the cross-q
+  // k_proj1 launch and its boundary cost (turbo step graph 0.274 -> 0.300 ms)
   static bool xq_proj1_on() {
     static const bool on = [] {
       const char* e = tune_env("WHISPER_HIP_XQP1");
-      return !(e && e[0] == '0');
+      return e && e[0] == '1';
     }();
     return on;
   }
