@@ -60,8 +60,9 @@ def parse():
     p.add_argument("--dtype", default="fp16")
     p.add_argument("--max-windows", type=int, default=20)
     p.add_argument("--cpu-baseline", type=int, default=1)
-    p.add_argument("--cpu-steps", type=int, default=0,
-                   help="CPU baseline: beam decoder steps of its window (0 = the whole 224-step window)")
+    p.add_argument("--cpu-steps", type=int, default=48,
+                   help="CPU baseline: beam decoder steps of its window, the step part scaled to the window's 224 "
+                        "(a bounded sample: ~20-25 s of CPU work on 16 cores; 0 = the whole 224-step window, ~90 s)")
     p.add_argument("--dump", default="", help="write the last step's segments (tokens, avg_logprob) as JSON")
     p.add_argument("--word-timestamps", type=int, default=0,
                    help="config 5: transcribe(word_timestamps=True) (alignment + DTW on the GPU per window)")

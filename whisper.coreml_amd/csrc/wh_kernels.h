@@ -68,6 +68,7 @@ struct XQPart {
   // with qx the LayerNorm'd rows [rows][n] and qw = W_q [n][n] (T); q / part unused
   const void* qx = nullptr;
   const void* qw = nullptr;
+  const void* qwf = nullptr;  // W_q in fragment order (launch_wq_frag), read instead of qw when set
   // the single-window step (k_proj1 layers): qx is the fp32 residual rows and the kernel
   // computes their LayerNorm (ln_g, ln_b, ln_eps) itself — no cross-q k_proj1 launch
   const float* ln_g = nullptr;
@@ -80,6 +81,10 @@ struct XQPart {
 inline bool xattn_fused_q(int n, int rows_per_window, int elem_size) {
   return elem_size == 2 && n == 1280 && rows_per_window >= 1 && rows_per_window <= 8;
 }
+// W_q [n][n] (fp16) -> the in-kernel query projection's fragment order: 16-B chunk
+// ((((h * 4 + c) * 2 + kh) * (n / 64) + s) * 64 + lane) holds row h * 64 + 16 c + (lane & 15),
+// columns kh * n / 2 + 32 s + 8 (lane >> 4) .. + 7 (a wave's k-step s is 1 KB contiguous)
+void launch_wq_frag(const void* w, void* f, int n, hipStream_t st);
 constexpr int XREC = 16 * 64 + 32;  // floats per segment record: O[16][64], m[16], l[16]
 // step cross-attention (k_xattn_seg): one softmax partial per 64-key tile, at most
 // XS_NSP tiles per (window, head) pair (Tk <= 1536), at most XS_QP pairs per workgroup

@@ -1633,9 +1633,15 @@ WH_DEV void xq_project(const XQPart& xq, int pa, int plast, int cnt, const int* 
   constexpr bool W_FIRST = QV >= 4;
   Frag<T> wf[QK];
   auto load_w = [&](int h) {
-    const T* wp = reinterpret_cast<const T*>(xq.qw) + (int64_t)(h * 64 + c * 16 + r) * N + kh * QK * 32 + 8 * g;
+    if (xq.qwf) {  // fragment order (launch_wq_frag): each k-step one 1 KB contiguous wave load
+      const T* wp = reinterpret_cast<const T*>(xq.qwf) + ((int64_t)((h * 4 + c) * 2 + kh) * QK * 64 + lane) * 8;
 #pragma unroll
-    for (int s = 0; s < QK; ++s) frag_load_stream(wf[s], wp + s * 32);
+      for (int s = 0; s < QK; ++s) frag_load_stream(wf[s], wp + s * 512);
+    } else {
+      const T* wp = reinterpret_cast<const T*>(xq.qw) + (int64_t)(h * 64 + c * 16 + r) * N + kh * QK * 32 + 8 * g;
+#pragma unroll
+      for (int s = 0; s < QK; ++s) frag_load_stream(wf[s], wp + s * 32);
+    }
   };
   if constexpr (W_FIRST) {
     load_w(q_h[0]);
@@ -2169,6 +2175,18 @@ bool xattn_l2_ranges(int nwin, int H, int max_rows, L2Prefetch* pf) {
     pf->hi[x] = (int)((s1 - 1) / nsp) / nwin + 1;
   }
   return true;
+}
+
+__global__ __launch_bounds__(256) void k_wq_frag(const half_t* __restrict__ w, half_t* __restrict__ f, int n) {
+  const int QK = n / 64, total = n * n / 8;
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < total; i += gridDim.x * 256) {
+    const int l = i % 64, t0 = i / 64, s = t0 % QK, t1 = t0 / QK, kh = t1 % 2, t2 = t1 / 2, c = t2 % 4, h = t2 / 4;
+    const int row = h * 64 + c * 16 + (l & 15), col = kh * (n / 2) + 32 * s + 8 * (l >> 4);
+    *reinterpret_cast<float4_t*>(f + (int64_t)i * 8) = *reinterpret_cast<const float4_t*>(w + (int64_t)row * n + col);
+  }
+}
+void launch_wq_frag(const void* w, void* f, int n, hipStream_t st) {
+  k_wq_frag<<<256, 256, 0, st>>>(reinterpret_cast<const half_t*>(w), reinterpret_cast<half_t*>(f), n), wh_launched("k_wq_frag");
 }
 
 template <typename T>

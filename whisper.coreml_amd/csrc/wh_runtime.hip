@@ -101,6 +101,9 @@ template <typename T>
 struct DecLayer {
   float *ln1_g, *ln1_b, *bqkv, *bo, *lnx_g, *lnx_b, *bqx, *box, *ln2_g, *ln2_b, *b1, *b2;
   T *wqkv, *wo, *wqx, *wox, *w1, *w2;
+  // round 6: W_q in the in-kernel query projection's fragment order (xq_project: each wave's
+  // 16 B-per-lane loads are 1 KB contiguous), fp16 contexts whose shape xattn_fused_q serves
+  T* wqx_f = nullptr;
 };
 
 struct Timer {
@@ -333,6 +336,9 @@ struct Ctx : public wh_ctx {
     }
     add(n, 4); add(n, 4);
     add(2 * Ld * n * n, sizeof(T)); add(2 * Ld * n, 4);
+    const bool wq_frag = xattn_fused_q(n, 1, (int)sizeof(T));
+    if (wq_frag)
+      for (int l = 0; l < Ld; ++l) add(n * n, sizeof(T));
     HIPCHK(hipMalloc(&wbase, wb));
     HIPCHK(hipMemset(wbase, 0, wb));
     wa.base = (char*)wbase;
@@ -355,7 +361,9 @@ struct Ctx : public wh_ctx {
     }
     ln_g = fk(n); ln_b = fk(n);
     ckv_w = tk(2 * Ld * n * n); ckv_b = fk(2 * Ld * n);
-    if (!ckv_b) return fail(-3, "weight arena overflow");
+    if (wq_frag)
+      for (auto& e : dec) e.wqx_f = tk(n * n);
+    if (!ckv_b || (wq_frag && !dec.back().wqx_f)) return fail(-3, "weight arena overflow");
     expected = 5 + La * 15 + 2 + 2 + Ld * 24 + 2;
     // ---------------- activations
     const int WE = std::min(Wcap, enc_chunk());
@@ -571,6 +579,11 @@ struct Ctx : public wh_ctx {
   int finalize() override {
     if (loaded.size() != expected)
       return fail(-6, "loaded " + std::to_string(loaded.size()) + " of " + std::to_string(expected) + " tensors");
+    // the fragment-ordered W_q copies (after the 0.125 query scale was folded in at load)
+    for (auto& e : dec)
+      if (e.wqx_f) launch_wq_frag(e.wqx, e.wqx_f, ns, st);
+    HIPCHK(hipStreamSynchronize(st));
+    HIPCHK(hipGetLastError());
     HIPCHK(hipDeviceSynchronize());
     finalized = true;
     return 0;
@@ -949,6 +962,7 @@ struct Ctx : public wh_ctx {
       if (skinny && xq_proj_active(ancG)) {
         // round 6: no cross-q launch; k_xattn_seg projects the LayerNorm'd rows itself
         xq.qx = xn_d; xq.qw = e.wqx; xq.bias = e.bqx;
+        if (xq_frag_on()) xq.qwf = e.wqx_f;
       } else if (skinny && xq_fused) {
         int ks = 0;
         TRY(partial(xn_d, n, e.wqx, R, n, n, &ks));
@@ -1101,6 +1115,7 @@ struct Ctx : public wh_ctx {
         // round 6: no cross-q k_proj1 launch; the cross-attention normalises the window's
         // fp32 rows and projects its query itself
         xq.qx = xc; xq.qw = e.wqx; xq.bias = e.bqx; xq.ln_g = e.lnx_g; xq.ln_b = e.lnx_b; xq.ln_eps = 1e-5f;
+        if (xq_frag_on()) xq.qwf = e.wqx_f;
       } else {
         g = GemmArgs();
         g.W = e.wqx; g.bias = e.bqx; g.M = R; g.N = n; g.K = n;
@@ -1462,6 +1477,14 @@ struct Ctx : public wh_ctx {
   static bool xq_proj_on() {
     static const bool on = [] {
       const char* e = tune_env("WHISPER_HIP_XQP");
+      return !(e && e[0] == '0');
+    }();
+    return on;
+  }
+  // the fragment-ordered W_q copy for it (WHISPER_HIP_XQ_FRAG=0: the [n][n] rows, A/B)
+  static bool xq_frag_on() {
+    static const bool on = [] {
+      const char* e = tune_env("WHISPER_HIP_XQ_FRAG");
       return !(e && e[0] == '0');
     }();
     return on;
@@ -1859,6 +1882,7 @@ struct Ctx : public wh_ctx {
               // or projected in the kernel (as the step does): from xn_d, or (single window)
               // from the fp32 rows with the LayerNorm in the kernel
               xq.qw = e.wqx; xq.bias = e.bqx;
+              if (xq_frag_on()) xq.qwf = e.wqx_f;
               if (p1_active(R, cur_nwin)) {
                 xq.qx = x_d; xq.ln_g = e.lnx_g; xq.ln_b = e.lnx_b;
               } else {
