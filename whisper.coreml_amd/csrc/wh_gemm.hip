@@ -795,6 +795,37 @@ __global__ __launch_bounds__(512) void k_vocab1(GemmArgs a) {
   CT_END(CT_VOCAB);
 }
 
+// the vocabulary kernels' epilogue: the workgroup's tiles transposed through LDS (the staged
+// rows of X are dead), so each store instruction writes 1 KB of one logit row instead of 16
+// rows x 64 B (the per-lane form: 7.5 us of k_vocab_2p's epilogue at 100 rows, this ~3)
+template <int MT, int NW>
+WH_DEV void vocab_store_tr(const GemmArgs& a, const float4_t (&acc)[MT], float* ot, int t0, int t1, bool act, int tid,
+                           int wave, int r, int g) {
+  constexpr int OTW = NW * 16 + 4;  // floats per staged row (+4: rows 4 banks apart)
+  __syncthreads();  // every wave is done with the rows of X
+  if (act) {
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+      const int m = mt * 16 + r;
+      if (m < a.M) *reinterpret_cast<float4_t*>(ot + m * OTW + wave * 16 + 4 * g) = acc[mt];
+    }
+  }
+  __syncthreads();
+  const auto rs = wt_rsrc(a.out_f32);
+  const int c0 = t0 * 16, nc = min(t1 * 16, a.N) - c0, nc4 = (nc + 3) >> 2;
+  for (int i = tid; i < a.M * nc4; i += NW * 64) {
+    const int m = i / nc4, c = 4 * (i - m * nc4), n = c0 + c;
+    const float4_t v = *reinterpret_cast<const float4_t*>(ot + m * OTW + c);
+    if (c + 3 < nc) {
+      wt_store4(rs, (m * a.ldo + n) * 4, v);
+    } else {
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        if (c + e < nc) wt_store1(rs, (m * a.ldo + n + e) * 4, v[e]);
+    }
+  }
+}
+
 // ============================================================ vocabulary projection, 33-112 rows
 // The decoder step's logits for a whole batch (20 windows x 5 beams = 100 rows) against
 // the token embedding (133 MB fp16): every row is resident in LDS, HALF of K at a time
@@ -898,33 +929,7 @@ __global__ __launch_bounds__(1024) void k_vocab_2p(GemmArgs a) {
   }
   CT_MARK(CT_VOCAB, 1);  // the MFMAs issued: the epilogue starts
   if constexpr (TR) {
-    // the workgroup's tiles transposed through LDS (X is dead): each store instruction
-    // writes 1 KB of one logit row instead of 16 rows x 64 B (the per-lane form below:
-    // 7.5 us of epilogue at 100 rows, this ~3)
-    constexpr int OTW = NW * 16 + 4;  // floats per staged row (+4: rows 4 banks apart)
-    float* ot = reinterpret_cast<float*>(xs2);
-    __syncthreads();  // every wave is done with the rows of X
-    if (act) {
-#pragma unroll
-      for (int mt = 0; mt < MT; ++mt) {
-        const int m = mt * 16 + r;
-        if (m < a.M) *reinterpret_cast<float4_t*>(ot + m * OTW + wave * 16 + 4 * g) = acc[mt];
-      }
-    }
-    __syncthreads();
-    const auto rs = wt_rsrc(a.out_f32);
-    const int c0 = t0 * 16, nc = min(t1 * 16, a.N) - c0, nc4 = (nc + 3) >> 2;
-    for (int i = tid; i < a.M * nc4; i += 1024) {
-      const int m = i / nc4, c = 4 * (i - m * nc4), n = c0 + c;
-      const float4_t v = *reinterpret_cast<const float4_t*>(ot + m * OTW + c);
-      if (c + 3 < nc) {
-        wt_store4(rs, (m * a.ldo + n) * 4, v);
-      } else {
-#pragma unroll
-        for (int e = 0; e < 4; ++e)
-          if (c + e < nc) wt_store1(rs, (m * a.ldo + n + e) * 4, v[e]);
-      }
-    }
+    vocab_store_tr<MT, NW>(a, acc, reinterpret_cast<float*>(xs2), t0, t1, act, tid, wave, r, g);
     CT_END(CT_VOCAB);
     return;
   }
@@ -957,6 +962,118 @@ __global__ __launch_bounds__(1024) void k_vocab_2p(GemmArgs a) {
       }
     }
   }
+  CT_END(CT_VOCAB);
+}
+
+// ============================================================ vocabulary projection, one pass over K
+// Round 6: k_vocab_2p's tiles, waves and k-step order with ONE pass
+// over K.  k_vocab_2p's first pass over K took ~22 us and its second ~9 whichever half went
+// first (profiles/r05/vocab_pass_order.txt): the first pulls whole 2560-B embedding rows
+// through the memory side and the second re-reads its half from there.  Here each wave
+// streams its 16 weight rows front to back once.  LDS holds X k-step-major: slot s =
+// [rows][32 halves] (64 B per row, a fragment read is 1 KB contiguous), 24 slots = k-steps
+// 0..23 staged up front; k-steps 24..39 refill slots 0..15 once every wave is past k-step
+// 15 (their loads issued a chunk earlier, ahead of that chunk's weight loads, so the LDS
+// writes wait on nothing the next MFMAs do not), with a second barrier before k-step 24.
+// Accumulation order per 16 x 16 block = ascending k-steps, as k_vocab_2p: bit-identical
+// logits.  Needs 24 x M x 64 B of LDS (M <= 106).  Measured: no faster than k_vocab_2p
+// (the weights stream at ~4.4 TB/s in both, profiles/r06/ab_vocab_1p_kco.txt) — the first
+// pass's ~22 us was the HBM stream, not a pass effect; tuning build only (WHISPER_HIP_V1P=1).  GATHER: rows of X named by a.x_rows (a
+// template choice: a wave-uniform pointer test per staging load made hipcc wait on each)
+constexpr int V1P_SLOTS = 24;
+template <int MT, bool GATHER>
+__global__ __launch_bounds__(1024) void k_vocab_1p(GemmArgs a) {
+  CT_MARK(CT_VOCAB, 0);
+  constexpr int NW = 16, VC = 4, DEPTH = 3, K = 1280, S = K / 32, SL = V1P_SLOTS, SR = S - SL, NCH = S / VC;
+  static_assert(S % VC == 0 && SR % VC == 0 && SR <= SL, "chunk / slot geometry");
+  constexpr int C_FREE = SR / VC;       // first chunk after the refilled slots' last use (k-steps 0..SR-1)
+  constexpr int C_REFILL = SL / VC;     // first chunk that reads refilled slots (k-step SL)
+  extern __shared__ __attribute__((aligned(16))) char xs1[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = lane & 15, g = lane >> 4;
+  const int M = a.M, slotB = M * 64;
+  const int nt = (a.N + 15) / 16;
+  const int t0 = range_split(blockIdx.x, nt, gridDim.x), t1 = range_split(blockIdx.x + 1, nt, gridDim.x);
+  const int tile = t0 + wave;
+  const bool act = tile < t1;
+  const half_t* X = reinterpret_cast<const half_t*>(a.X);
+  const int* const xrows = a.x_rows;
+  const half_t* wrow = reinterpret_cast<const half_t*>(a.W) + (int64_t)min(tile * 16 + r, a.N - 1) * K + 8 * g;
+  float4_t acc[MT];
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt) acc[mt] = (float4_t){0.f, 0.f, 0.f, 0.f};
+  Frag<half_t> wbuf[DEPTH][VC];
+  auto load_chunk = [&](int c, Frag<half_t>(&wf)[VC]) {
+    const half_t* wp = wrow + c * VC * 32;
+#pragma unroll
+    for (int u = 0; u < VC; ++u) frag_load_stream(wf[u], wp + u * 32);
+  };
+  // chunk i of a k-step range: (k-step ks0 + i / (M*4), row, 16-B column) <- X (32-bit
+  // buffer offsets: one register per in-flight chunk, not a 64-bit address pair)
+  const auto rx = wt_rsrc(X);
+  auto src = [&](Frag<half_t>& f, int ks0, int i) {
+    const int kk = i / (M * 4), rem = i - kk * M * 4, row = rem >> 2, col = rem & 3;
+    const int xr = GATHER ? xrows[row] : row;
+    frag_load_buf(f, rx, (xr * a.ldx + (ks0 + kk) * 32 + col * 8) * 2);
+  };
+  if (act) {
+#pragma unroll
+    for (int c = 0; c < DEPTH - 1; ++c) load_chunk(c, wbuf[c]);
+  }
+  {
+    constexpr int SU = (106 * SL * 4 + 1023) / 1024;
+    const int tot = M * SL * 4;
+    Frag<half_t> tmp[SU];
+#pragma unroll
+    for (int u = 0; u < SU; ++u) src(tmp[u], 0, min(tid + 1024 * u, tot - 1));
+#pragma unroll
+    for (int u = 0; u < SU; ++u) {
+      const int i = tid + 1024 * u;
+      if (i < tot) *reinterpret_cast<half8_t*>(xs1 + i * 16) = tmp[u].v;  // slot kk, row, col: i * 16
+    }
+  }
+  __syncthreads();
+  // the refill in two parts (the whole refill live across a chunk's MFMAs spilled at MT 7):
+  // part j's loads issued at chunk C_FREE - 1 + j ahead of that chunk's weight loads, its LDS
+  // writes at chunk C_FREE + j (part 0 after the barrier that frees the slots)
+  constexpr int RU = (106 * SR * 4 + 1023) / 1024, RU0 = (RU + 1) / 2;
+  static_assert(C_FREE + 1 < C_REFILL, "two refill parts between the barriers");
+  const int rtot = M * SR * 4;
+  Frag<half_t> rf[RU0];
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int u0 = j ? RU0 : 0, u1 = j ? RU : RU0;
+      if (c == C_FREE + j) {
+        if (j == 0) __syncthreads();  // every wave is past k-step SR - 1: slots 0..SR-1 are free
+#pragma unroll
+        for (int u = u0; u < u1; ++u) {
+          const int i = tid + 1024 * u;
+          if (i < rtot) *reinterpret_cast<half8_t*>(xs1 + i * 16) = rf[u - u0].v;
+        }
+      }
+      if (c == C_FREE - 1 + j) {
+#pragma unroll
+        for (int u = u0; u < u1; ++u) src(rf[u - u0], SL, min(tid + 1024 * u, rtot - 1));
+      }
+    }
+    if (c == C_REFILL) __syncthreads();  // the refilled slots written
+    if (act) {
+      if (c + DEPTH - 1 < NCH) load_chunk(c + DEPTH - 1, wbuf[(c + DEPTH - 1) % DEPTH]);
+#pragma unroll
+      for (int u = 0; u < VC; ++u) {
+        const int ks = c * VC + u, slot = ks < SL ? ks : ks - SL;
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) {
+          Frag<half_t> xf;
+          frag_load(xf, reinterpret_cast<const half_t*>(xs1 + slot * slotB + min(mt * 16 + r, M - 1) * 64 + 16 * g));
+          mfma_step(acc[mt], wbuf[c % DEPTH][u], xf);
+        }
+      }
+    }
+  }
+  CT_MARK(CT_VOCAB, 1);  // the MFMAs issued: the epilogue starts
+  vocab_store_tr<MT, NW>(a, acc, reinterpret_cast<float*>(xs1), t0, t1, act, tid, wave, r, g);
   CT_END(CT_VOCAB);
 }
 
@@ -1238,8 +1355,24 @@ int launch_gemm_tiles(const GemmArgs& a, int epi, int tile_sel, hipStream_t st) 
       const int nt = (a.N + 15) / 16;
       const int grid = std::max((nt + 15) / 16, std::min(256, nt));
       const int lds = a.M * (a.K + 16);  // rows x (K / 2 halves x 2 B + 16)
+      // tuning build, WHISPER_HIP_V1P=1: k_vocab_1p (one pass over K) when its 24 k-step
+      // slots fit (M <= 106).  Measured equal: weights-in to epilogue start ~30 us either way
+      // (20 windows: step 3.186 / 3.187 ms at 12 tokens, profiles/r06/ab_vocab_1p_kco.txt)
+      const char* v1e = tune_env("WHISPER_HIP_V1P");
+      const bool v1p = v1e && v1e[0] == '1' && tr && V1P_SLOTS * a.M * 64 <= 160 * 1024;
       auto go = [&](auto mtc) {
         constexpr int MTV = decltype(mtc)::value;
+        if (v1p) {
+          const int lds1 = std::max(V1P_SLOTS * a.M * 64, a.M * (16 * 16 + 4) * 4);
+          static bool attr1 = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_vocab_1p<MTV, true>),
+                                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) == hipSuccess &&
+                              hipFuncSetAttribute(reinterpret_cast<const void*>(&k_vocab_1p<MTV, false>),
+                                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) == hipSuccess;
+          if (!attr1) return -5;
+          if (a.x_rows) k_vocab_1p<MTV, true><<<grid, 1024, lds1, st>>>(a), wh_launched("k_vocab_1p");
+          else k_vocab_1p<MTV, false><<<grid, 1024, lds1, st>>>(a), wh_launched("k_vocab_1p");
+          return 0;
+        }
         static bool attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_vocab_2p<MTV, 2>),
                                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) == hipSuccess &&
                            hipFuncSetAttribute(reinterpret_cast<const void*>(&k_vocab_2p<MTV, 3>),

@@ -166,6 +166,8 @@ struct GemmArgs;
 bool vocab_select_on();
 int self_attn_grp_mode();
 bool self_attn_pipe_on();
+bool self_attn_kco_on();  // the coalesced-K self-attention passes (round 6)
+int self_attn_kco_min();   // ... from this many cached keys on
 int launch_vocab_select(const GemmArgs& a, const DecState& s, const DecOpts& o, const MergeEmbed& em, float* rec,
                         int* cnt, hipStream_t st);
 constexpr size_t VS_REC_FLOATS = 8 * 2 * 256 * 32;  // k_vocab_sel records [rows][part][workgroup][32]

@@ -379,18 +379,63 @@ void launch_attn_enc(const T* qkv, int ld, int ns, int H, int Tlen, int nwin, in
   }
 }
 
+// One online-softmax pass of the coalesced-K self-attention (round 6): lane (kg, dc) holds
+// the 16-B chunk dc (dims dc .. dc+7) of keys key0 + 8u, u < NU, of both K and V (eight
+// lanes per 128-B row, so a load instruction covers whole rows); keys >= lim are masked.  A
+// key's score is its 8 chunk partials summed across the group's lanes with DPP (pairs, quads,
+// then the other quad: after the quad steps a quad's lanes agree, so the half-row mirror is a
+// partner; each step adds two operands equal for both lanes, so the 8 lanes hold the same
+// sum) and lands in the lanes whose V chunks it weights: no LDS hand-off of the weights.
+template <typename T, int NU>
+WH_DEV void kco_pass(const float (&qd8)[8], const Frag<T> (&k)[NU], const Frag<T> (&v)[NU], int key0, int lim,
+                     float& m, float& lsum, float (&o)[8]) {
+  constexpr int XOR1 = 0xB1, XOR2 = 0x4E, HALF_MIRROR = 0x141;  // quad_perm [1,0,3,2], [2,3,0,1]
+  float s[NU], mx = -INFINITY;
+#pragma unroll
+  for (int u = 0; u < NU; ++u) {
+    float a = 0.f;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) a += qd8[e] * to_f32(k[u].v[e]);
+    a += dpp_f<XOR1>(a);
+    a += dpp_f<XOR2>(a);
+    a += dpp_f<HALF_MIRROR>(a);
+    s[u] = a;
+    if (key0 + 8 * u < lim) mx = fmaxf(mx, a);
+  }
+  mx = fmaxf(mx, dpp_f<DPP_ROR8>(mx));
+  mx = xor16_max(mx);
+  mx = xor32_max(mx);
+  const float mn = fmaxf(m, mx), scale = __expf(m - mn);
+  m = mn;
+  float es = 0.f;
+#pragma unroll
+  for (int u = 0; u < NU; ++u) {
+    s[u] = key0 + 8 * u < lim ? __expf(s[u] - mn) : 0.f;
+    es += s[u];
+  }
+  lsum = lsum * scale + xor32_sum(xor16_sum(xor8_sum(es)));
+#pragma unroll
+  for (int e = 0; e < 8; ++e) o[e] *= scale;
+#pragma unroll
+  for (int u = 0; u < NU; ++u)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] += s[u] * to_f32(v[u].v[e]);
+}
+
 // ============================================================ decoder self-attention
 // One wave per (row, head).  Keys = positions 0..pos of the row's sequence; position
 // p < pos lives in beam slot anc[win][slot][p] (beam reorder by index indirection,
 // no KV copies), position pos in the row's own slot.  Cache: [win][slot][head][ctx][64].
 // PIPE (fp16, round 4): 64-key passes with the next pass's loads in flight, as
-// k_self_attn_qkv<T, true>
-template <typename T, bool PIPE = false>
+// k_self_attn_qkv<T, true>.  KCO (fp16, round 6): the 128-key passes with K read like V
+// (kco_pass)
+template <typename T, bool PIPE = false, bool KCO = false>
 __global__ __launch_bounds__(64) void k_self_attn(const T* __restrict__ q, int ldq, const T* __restrict__ kc,
                                                   const T* __restrict__ vc, const int* __restrict__ row_win,
                                                   const int* __restrict__ row_slot, const int* __restrict__ row_pos,
                                                   const int* __restrict__ anc, int anc_beams, int nbeam, int H,
-                                                  int ctx, T* __restrict__ out, int ldo) {  CT_MARK(CT_SELF_ATTN, 0);
+                                                  int ctx, T* __restrict__ out, int ldo, int kco_min = 0) {
+  CT_MARK(CT_SELF_ATTN, 0);
 
   __shared__ float sc[512];
   __shared__ int slot_of[512];
@@ -491,6 +536,55 @@ __global__ __launch_bounds__(64) void k_self_attn(const T* __restrict__ q, int l
     }
     CT_END(CT_SELF_ATTN);
     return;
+  }
+  if constexpr (sizeof(T) == 2 && KCO) {
+    if (pos + 1 > kco_min) {  // (one 128-key pass below: the lane-per-key form)
+      int sv[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) sv[i] = an[min(lane + 64 * i, ctx - 1)];
+      qs[lane] = to_f32(q_lane);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int pp = lane + 64 * i;
+        if (pp <= pos) slot_of[pp] = (pp == pos ? sl : sv[i]) * slotB;
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // one wave: its own LDS writes
+      const int kg = lane >> 3, dc = (lane & 7) * 8;
+      float qd8[8], m = -INFINITY, lsum = 0.f, o[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        qd8[e] = qs[dc + e];
+        o[e] = 0.f;
+      }
+      for (int p0 = 0; p0 <= pos; p0 += 128) {
+        Frag<T> k[16], v[16];
+        int off[16];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) {
+          const int pc = min(p0 + kg + 8 * u, pos);
+          off[u] = baseB + slot_of[pc] + pc * ROWB + dc * TB;
+        }
+#pragma unroll
+        for (int u = 0; u < 16; ++u) frag_load_buf(k[u], rk, off[u]);
+#pragma unroll
+        for (int u = 0; u < 16; ++u) frag_load_buf(v[u], rv, off[u]);
+        kco_pass<T, 16>(qd8, k, v, p0 + kg, pos + 1, m, lsum, o);
+      }
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        o[e] = xor8_sum(o[e]);
+        o[e] = xor16_sum(o[e]);
+        o[e] = xor32_sum(o[e]);
+      }
+      if (kg == 0) {
+        const float inv = 1.f / lsum;
+        T* op = out + (int64_t)row * ldo + h * 64 + dc;
+        store4(op, o[0] * inv, o[1] * inv, o[2] * inv, o[3] * inv);
+        store4(op + 4, o[4] * inv, o[5] * inv, o[6] * inv, o[7] * inv);
+      }
+      CT_END(CT_SELF_ATTN);
+      return;
+    }
   }
   if constexpr (sizeof(T) == 2) {
     // round 3 (fp16): the k_self_attn_qkv schedule — the ancestry of every context
@@ -652,6 +746,11 @@ void launch_self_attn(const T* q, int ldq, const T* kc, const T* vc, const int* 
     return e && e[0] == '1';
   }();
   if constexpr (sizeof(T) == 2) {
+    if (self_attn_kco_on()) {
+      k_self_attn<T, false, true><<<dim3(rows, H), 64, 0, st>>>(q, ldq, kc, vc, rw, rs, rp, anc, anc_beams, nbeam, H,
+                                                                ctx, out, ldo, self_attn_kco_min()), wh_launched("k_self_attn");
+      return;
+    }
     if (pipe) {
       k_self_attn<T, true><<<dim3(rows, H), 64, 0, st>>>(q, ldq, kc, vc, rw, rs, rp, anc, anc_beams, nbeam, H, ctx, out,
                                                          ldo), wh_launched("k_self_attn");
@@ -676,13 +775,19 @@ void launch_self_attn(const T* q, int ldq, const T* kc, const T* vc, const int* 
 // the current pass is computed (two register buffers of 8 K + 8 V fragments), q read from
 // LDS: at long contexts the passes' round trips overlap instead of adding up (the step's
 // growth over the decode is those round trips, profiles/r04/self_attn_grp64_ab.txt).
+// PIPE 3 (round 6): the PIPE 1 passes with K read like V — lane (kg, dc) holds the 16-B
+// chunk dc of keys kg + 8u, eight lanes per 128-B key row — so one load instruction covers
+// 8 whole rows (the lane-per-key form touched 64 rows, 16 B of each, per instruction, and
+// the rows' other chunks came back by later instructions from wherever the lines still
+// were).  A key's score is its 8 chunk partials summed across the group's lanes (DPP) and
+// lands in the lanes whose V chunks it weights: no LDS hand-off of the probabilities.
 template <typename T, int PIPE = 0, typename S = float>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void k_self_attn_qkv(const S* __restrict__ part, int nsplit, int64_t part_stride,
                                                       const float* __restrict__ bqkv, int ns, T* __restrict__ kc,
                                                       T* __restrict__ vc, const int* __restrict__ row_win,
                                                       const int* __restrict__ row_slot, const int* __restrict__ row_pos,
                                                       const int* __restrict__ anc, int anc_beams, int nbeam, int H,
-                                                      int ctx, T* __restrict__ out, int ldo) {
+                                                      int ctx, T* __restrict__ out, int ldo, int kco_min = 0) {
   __shared__ float sc[512];
   __shared__ int slot_of[512];
   __shared__ float qs[64], vs[64];
@@ -760,7 +865,23 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void
     float m = s_cur, lsum = 0.f, o[8];
 #pragma unroll
     for (int e = 0; e < 8; ++e) o[e] = 0.f;
-    auto load = [&](int p0, Frag<T>(&k)[8], Frag<T>(&v)[8]) {
+    float qd8[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) qd8[e] = qs[dc + e];
+    auto load = [&](auto kc, int p0, Frag<T>(&k)[8], Frag<T>(&v)[8]) {
+      if constexpr (decltype(kc)::value) {
+        int off[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const int pc = min(p0 + kg + 8 * u, plast);
+          off[u] = baseB + slot_of[pc] + pc * ROWB + dc * TB;
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) frag_load_buf(k[u], rk, off[u]);
+#pragma unroll
+        for (int u = 0; u < 8; ++u) frag_load_buf(v[u], rv, off[u]);
+        return;
+      }
       const int pa = min(p0 + lane, plast);
       const int ra = baseB + slot_of[pa] + pa * ROWB;
 #pragma unroll
@@ -771,7 +892,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void
         frag_load_buf(v[u], rv, baseB + slot_of[pc] + pc * ROWB + dc * TB);
       }
     };
-    auto pass = [&](int p0, const Frag<T>(&k)[8], const Frag<T>(&v)[8]) {
+    auto pass = [&](auto kc, int p0, const Frag<T>(&k)[8], const Frag<T>(&v)[8]) {
+      if constexpr (decltype(kc)::value) {
+        kco_pass<T, 8>(qd8, k, v, p0 + kg, pos, m, lsum, o);
+        return;
+      }
       float sa = 0.f;
 #pragma unroll
       for (int c = 0; c < 8; ++c) {
@@ -797,33 +922,44 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void
         for (int e = 0; e < 8; ++e) o[e] += pw * to_f32(v[u].v[e]);
       }
     };
-    Frag<T> ka[8], va[8], kb[8], vb[8];
-    if (pos > 0) load(0, ka, va);
-    int p0 = 0;
-    if constexpr (PIPE >= 2) {
-      // two passes in flight ahead of the one computed (three register sets, <= 256
-      // VGPRs: still two waves per SIMD, every (row, head) wave resident at once); the
-      // passes are computed in the same order, so the result is bit-identical to PIPE 1
-      Frag<T> kx[8], vx[8];
-      if (pos > 64) load(64, kb, vb);
-      for (; p0 + 128 < pos; p0 += 192) {
-        load(p0 + 128, kx, vx);
-        pass(p0, ka, va);
-        if (p0 + 192 < pos) load(p0 + 192, ka, va);
-        pass(p0 + 64, kb, vb);
-        if (p0 + 256 < pos) load(p0 + 256, kb, vb);
-        pass(p0 + 128, kx, vx);
+    // the coalesced-K passes (PIPE 3) from kco_min cached keys on: below that (one pass)
+    // the lane-per-key form measured faster (20-window step 3.186 -> 3.198 ms at 12
+    // tokens, 3.475 -> 3.448 at 162, profiles/r06/ab_self_attn_kco.txt)
+    auto run = [&](auto kc) {
+      Frag<T> ka[8], va[8], kb[8], vb[8];
+      if (pos > 0) load(kc, 0, ka, va);
+      int p0 = 0;
+      if constexpr (PIPE == 2) {
+        // two passes in flight ahead of the one computed (three register sets, <= 256
+        // VGPRs: still two waves per SIMD, every (row, head) wave resident at once); the
+        // passes are computed in the same order, so the result is bit-identical to PIPE 1
+        Frag<T> kx[8], vx[8];
+        if (pos > 64) load(kc, 64, kb, vb);
+        for (; p0 + 128 < pos; p0 += 192) {
+          load(kc, p0 + 128, kx, vx);
+          pass(kc, p0, ka, va);
+          if (p0 + 192 < pos) load(kc, p0 + 192, ka, va);
+          pass(kc, p0 + 64, kb, vb);
+          if (p0 + 256 < pos) load(kc, p0 + 256, kb, vb);
+          pass(kc, p0 + 128, kx, vx);
+        }
+        if (p0 < pos) pass(kc, p0, ka, va);
+        if (p0 + 64 < pos) pass(kc, p0 + 64, kb, vb);
+      } else {
+        for (; p0 + 64 < pos; p0 += 128) {
+          load(kc, p0 + 64, kb, vb);
+          pass(kc, p0, ka, va);
+          if (p0 + 128 < pos) load(kc, p0 + 128, ka, va);
+          pass(kc, p0 + 64, kb, vb);
+        }
+        if (p0 < pos) pass(kc, p0, ka, va);
       }
-      if (p0 < pos) pass(p0, ka, va);
-      if (p0 + 64 < pos) pass(p0 + 64, kb, vb);
+    };
+    if constexpr (PIPE == 3) {
+      if (pos > kco_min) run(std::true_type());
+      else run(std::false_type());
     } else {
-      for (; p0 + 64 < pos; p0 += 128) {
-        load(p0 + 64, kb, vb);
-        pass(p0, ka, va);
-        if (p0 + 128 < pos) load(p0 + 128, ka, va);
-        pass(p0 + 64, kb, vb);
-      }
-      if (p0 < pos) pass(p0, ka, va);
+      run(std::false_type());
     }
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
@@ -1191,6 +1327,23 @@ int self_attn_grp_mode() {
   }();
   return grp;
 }
+// the coalesced-K passes (PIPE 3) of the fp16-slab step form; WHISPER_HIP_SA_KCO=0 in the
+// tuning build: the lane-per-key K loads (PIPE 1)
+bool self_attn_kco_on() {
+  static const bool on = [] {
+    const char* e = tune_env("WHISPER_HIP_SA_KCO");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+// the cached-key count from which the coalesced-K passes run (tuning WHISPER_HIP_SA_KCO_MIN)
+int self_attn_kco_min() {
+  static const int v = [] {
+    const char* e = tune_env("WHISPER_HIP_SA_KCO_MIN");
+    return e ? atoi(e) : 64;
+  }();
+  return v;
+}
 bool self_attn_pipe_on() {
   static const bool pipe = [] {
     const char* e = tune_env("WHISPER_HIP_SA_PIPE");
@@ -1212,6 +1365,13 @@ int launch_self_attn_qkv(const float* part, int nsplit, int64_t part_stride, con
   if (slab_half) {
     if constexpr (sizeof(T) == 2) {
       if (self_attn_pipe_on() && !self_attn_grp_mode()) {
+        if (self_attn_kco_on()) {
+          k_self_attn_qkv<T, 3, half_t><<<rows * H, 64, 0, st>>>(reinterpret_cast<const half_t*>(part), nsplit,
+                                                                part_stride, bqkv, ns, kc, vc, rw, rs, rp, anc,
+                                                                anc_beams, nbeam, H, ctx, out, ldo,
+                                                                self_attn_kco_min()), wh_launched("k_self_attn_qkv");
+          return 0;
+        }
         k_self_attn_qkv<T, 1, half_t><<<rows * H, 64, 0, st>>>(reinterpret_cast<const half_t*>(part), nsplit,
                                                               part_stride, bqkv, ns, kc, vc, rw, rs, rp, anc,
                                                               anc_beams, nbeam, H, ctx, out, ldo), wh_launched("k_self_attn_qkv");
@@ -1250,7 +1410,11 @@ int launch_self_attn_qkv(const float* part, int nsplit, int64_t part_stride, con
         const char* e = tune_env("WHISPER_HIP_SA_DEPTH");
         return e && e[0] == '2' ? 2 : 1;
       }();
-      if (depth == 2)
+      if (self_attn_kco_on())
+        k_self_attn_qkv<T, 3><<<rows * H, 64, 0, st>>>(part, nsplit, part_stride, bqkv, ns, kc, vc, rw, rs, rp, anc,
+                                                      anc_beams, nbeam, H, ctx, out, ldo, self_attn_kco_min()),
+            wh_launched("k_self_attn_qkv");
+      else if (depth == 2)
         k_self_attn_qkv<T, 2><<<rows * H, 64, 0, st>>>(part, nsplit, part_stride, bqkv, ns, kc, vc, rw, rs, rp, anc,
                                                       anc_beams, nbeam, H, ctx, out, ldo), wh_launched("k_self_attn_qkv");
       else

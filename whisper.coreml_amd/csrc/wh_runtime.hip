@@ -1065,9 +1065,9 @@ struct Ctx : public wh_ctx {
     return std::string("proj=") + (p1 ? "k_proj1" : "k_proj") + ",xattn=k_xattn_seg" +
            (!p1 && xq_proj_active(group) ? "<qproj>" : p1 && xq_proj1_active(group) ? "<qproj+ln>" : "") +
            ",self_attn=" +
-           (p1 ? "k_self_attn"
+           (p1 ? (h && self_attn_kco_on() ? "k_self_attn<kco>" : "k_self_attn")
                : h && group >= 2 && self_attn_grp_mode() ? "k_self_attn_grp"
-                                                           : h && self_attn_pipe_on() ? "k_self_attn_qkv<pipe>"
+                                                           : h && self_attn_pipe_on() ? (self_attn_kco_on() ? "k_self_attn_qkv<pipe+kco>" : "k_self_attn_qkv<pipe>")
                                                                                       : "k_self_attn_qkv") +
            ",tail=" + (p1 && h && ns == 1280 && vocab_select_on() ? "k_vocab_sel" : "vocab+k_logit_part");
   }
