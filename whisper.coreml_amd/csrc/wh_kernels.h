@@ -85,6 +85,10 @@ inline bool xattn_fused_q(int n, int rows_per_window, int elem_size) {
 // ((((h * 4 + c) * 2 + kh) * (n / 64) + s) * 64 + lane) holds row h * 64 + 16 c + (lane & 15),
 // columns kh * n / 2 + 32 s + 8 (lane >> 4) .. + 7 (a wave's k-step s is 1 KB contiguous)
 void launch_wq_frag(const void* w, void* f, int n, hipStream_t st);
+// round-6 probe (tuning build): pull a layer's cross K / V blocks of nwin windows (slots from
+// win_slot, slot_bytes each, a multiple of 32 KB) through the memory side; nwg one-wave workgroups
+void launch_kv_pull(const void* ck, const void* cv, const int* win_slot, int nwin, int64_t slot_bytes, int nwg,
+                    unsigned* sink, hipStream_t st);
 constexpr int XREC = 16 * 64 + 32;  // floats per segment record: O[16][64], m[16], l[16]
 // step cross-attention (k_xattn_seg): one softmax partial per 64-key tile, at most
 // XS_NSP tiles per (window, head) pair (Tk <= 1536), at most XS_QP pairs per workgroup

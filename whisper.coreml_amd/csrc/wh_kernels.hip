@@ -2353,6 +2353,42 @@ void launch_wq_frag(const void* w, void* f, int n, hipStream_t st) {
   k_wq_frag<<<256, 256, 0, st>>>(reinterpret_cast<const half_t*>(w), reinterpret_cast<half_t*>(f), n), wh_launched("k_wq_frag");
 }
 
+// Round 6 probe (tuning build, WHISPER_HIP_XKV_PF=<workgroups>): pull one layer's cross-
+// attention K and V blocks of the batch's windows through the memory side on a second
+// stream beside the layer's launch chain, so that k_xattn_seg reads them from the Infinity
+// Cache (256 MiB; 157 MB at 20 windows) instead of HBM.  (Register loads folded into a
+// dummy word: hipcc copied the loop-carried registers and waited on every load.)
+__global__ __launch_bounds__(256) void k_kv_pull(const char* __restrict__ ck, const char* __restrict__ cv,
+                                                 const int* __restrict__ win_slot, int nwin, int64_t slot_bytes) {
+  // workgroup b: 32-KB pieces b, b + grid, ... of the windows' K then V blocks; each wave
+  // moves 8 KB of a piece by LDS-DMA into a 1-KB sink (no registers, nothing read back) and
+  // keeps at most 24 KB in flight (explicit vmcnt: the DMA's only consumer is the exit)
+  constexpr int64_t CH = 32768;
+  __shared__ __attribute__((aligned(16))) char sink[1024];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int cpb = (int)(slot_bytes / CH), total = 2 * nwin * cpb;
+  for (int c = blockIdx.x; c < total; c += gridDim.x) {
+    const int blk = c / cpb, w = blk >> 1;
+    int slot;  // a scalar load: a vector one would retire behind the DMA loads (vmcnt in order)
+    asm volatile("s_load_dword %0, %1, 0x0\n\ts_waitcnt lgkmcnt(0)" : "=s"(slot) : "s"(win_slot + w) : "memory");
+    const char* p = ((blk & 1) ? cv : ck) + (int64_t)slot * slot_bytes + (int64_t)(c - blk * cpb) * CH + tid * 16;
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+      __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)(p + u * 4096),
+                                       (__attribute__((address_space(3))) void*)(sink), 16, 0, 0);
+    asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA into the sink after the workgroup ends
+  (void)lane;
+}
+void launch_kv_pull(const void* ck, const void* cv, const int* win_slot, int nwin, int64_t slot_bytes, int nwg,
+                    unsigned* sink, hipStream_t st) {
+  (void)sink;
+  if (nwin <= 0 || nwg <= 0 || slot_bytes % 32768) return;
+  k_kv_pull<<<nwg, 256, 0, st>>>(reinterpret_cast<const char*>(ck), reinterpret_cast<const char*>(cv), win_slot, nwin,
+                                 slot_bytes), wh_launched("k_kv_pull");
+}
+
 template <typename T>
 void launch_cross_attn(const T* q, int ldq, const T* ck, const T* cv, int Tk, int H, int nsplit, int nwin,
                        const int* win_row0, const int* win_nrows, const int* win_slot, int64_t win_stride, float* po,

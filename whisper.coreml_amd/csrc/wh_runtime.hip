@@ -280,6 +280,12 @@ struct Ctx : public wh_ctx {
     if (gexec) rel(hipGraphExecDestroy(gexec), "hipGraphExecDestroy");
     if (graph) rel(hipGraphDestroy(graph), "hipGraphDestroy");
     if (st) rel(hipStreamDestroy(st), "hipStreamDestroy");
+    if (pst) {  // the tuning build's KV pull stream (kv_pull_setup)
+      rel(hipStreamSynchronize(pst), "hipStreamSynchronize(pull)");
+      rel(hipStreamDestroy(pst), "hipStreamDestroy(pull)");
+      for (auto& e : kv_ev) rel(hipEventDestroy(e), "hipEventDestroy(pull)");
+      rel(hipFree(kv_sink), "hipFree(pull sink)");
+    }
     if (wbase) rel(hipFree(wbase), "hipFree(weights)");
     if (abase) rel(hipFree(abase), "hipFree(activations)");
     if (d_audio) rel(hipFree(d_audio), "hipFree(audio)");
@@ -895,6 +901,41 @@ struct Ctx : public wh_ctx {
     return on;
   }
 
+  // round-6 probe, tuning build only: WHISPER_HIP_XKV_PF=<workgroups> pulls each layer's
+  // cross K / V through the memory side on a second stream (k_kv_pull), forked after the
+  // previous layer's cross-attention, joined at the end of the layers
+  static int xkv_pf_wg() {
+    static const int v = [] {
+      const char* e = tune_env("WHISPER_HIP_XKV_PF");
+      return e ? atoi(e) : 0;
+    }();
+    return v;
+  }
+  hipStream_t pst = nullptr;
+  std::vector<hipEvent_t> kv_ev;
+  unsigned* kv_sink = nullptr;
+  int kv_pull_setup() {
+    if (pst) return 0;
+    HIPCHK(hipStreamCreateWithFlags(&pst, hipStreamNonBlocking));
+    kv_ev.resize(Ld + 1);
+    for (auto& e : kv_ev) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    HIPCHK(hipMalloc((void**)&kv_sink, 256));
+    return 0;
+  }
+  int kv_pull(int l, int nwin, const int* wsl) {
+    HIPCHK(hipEventRecord(kv_ev[l], st));
+    HIPCHK(hipStreamWaitEvent(pst, kv_ev[l], 0));
+    const size_t n = ns;
+    launch_kv_pull(ckv + (size_t)(2 * l) * Wcap * TKP * n, ckv + (size_t)(2 * l + 1) * Wcap * TKP * n, wsl, nwin,
+                   (int64_t)TKP * n * sizeof(T), xkv_pf_wg(), kv_sink, pst);
+    return 0;
+  }
+  int kv_join() {
+    HIPCHK(hipEventRecord(kv_ev[Ld], pst));
+    HIPCHK(hipStreamWaitEvent(st, kv_ev[Ld], 0));
+    return 0;
+  }
+
   // out = act(xn W^T + b) for R rows (cross-attention query, MLP fc1): split-K
   // partial slabs + fixed-order reduce in step mode, the direct GEMM otherwise
   int proj(const T* W, const float* b, int R, int N, T* out, int gelu, bool skinny) {
@@ -931,6 +972,11 @@ struct Ctx : public wh_ctx {
     if (step && !qkmap && p1_active(R, nwin))
       return dec_layers_p1(R, rw, rs, rp, ancG, nwin, wr0, wnr, wsl, A);
     launch_layernorm<T>(x_d, xn_d, dec[0].ln1_g, dec[0].ln1_b, R, n, 1e-5f, nullptr, st);
+    const bool kvpf = skinny && nwin >= 2 && xkv_pf_wg() > 0;
+    if (kvpf) {
+      TRY(kv_pull_setup());
+      TRY(kv_pull(0, nwin, wsl));
+    }
     for (int l = 0; l < Ld; ++l) {
       auto& e = dec[l];
       if (skinny) {
@@ -978,11 +1024,13 @@ struct Ctx : public wh_ctx {
       const T* cv = ckv + (size_t)(2 * l + 1) * Wcap * TKP * n;
       launch_cross_attn<T>(q_d, n, ck, cv, 1500, nh, NSPLIT, nwin, wr0, wnr, wsl, (int64_t)TKP * n, po, pm, pl, att_d,
                            n, R, aqk, qkmap ? qkmap + l * nh : nullptr, qkrows, st, xq);
+      if (kvpf && l + 1 < Ld) TRY(kv_pull(l + 1, nwin, wsl));
       TRY(resid(att_d, n, e.wox, e.box, R, e.ln2_g, e.ln2_b));
       TRY(proj(e.w1, e.b1, R, 4 * n, hm_d, 1, skinny));
       const bool last = l + 1 == Ld;
       TRY(resid(hm_d, 4 * n, e.w2, e.b2, R, last ? ln_g : dec[l + 1].ln1_g, last ? ln_b : dec[l + 1].ln1_b));
     }
+    if (kvpf) TRY(kv_join());
     return 0;
   }
 
@@ -1454,6 +1502,7 @@ struct Ctx : public wh_ctx {
     if (gexec && key == graph_key) return 0;
     if (gexec) { hipGraphExecDestroy(gexec); gexec = nullptr; }
     if (graph) { hipGraphDestroy(graph); graph = nullptr; }
+    if (xkv_pf_wg() > 0) TRY(kv_pull_setup());  // (no stream / event creation or hipMalloc under capture)
     HIPCHK(hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal));
     const int rc = step_body();
     hipGraph_t g = nullptr;
