@@ -916,7 +916,15 @@ struct Ctx : public wh_ctx {
   unsigned* kv_sink = nullptr;
   int kv_pull_setup() {
     if (pst) return 0;
-    HIPCHK(hipStreamCreateWithFlags(&pst, hipStreamNonBlocking));
+    // WHISPER_HIP_XKV_PRIO=1: the pull stream at the device's greatest priority
+    const char* pe = tune_env("WHISPER_HIP_XKV_PRIO");
+    if (pe && pe[0] == '1') {
+      int lo = 0, hi = 0;
+      HIPCHK(hipDeviceGetStreamPriorityRange(&lo, &hi));
+      HIPCHK(hipStreamCreateWithPriority(&pst, hipStreamNonBlocking, hi));
+    } else {
+      HIPCHK(hipStreamCreateWithFlags(&pst, hipStreamNonBlocking));
+    }
     kv_ev.resize(Ld + 1);
     for (auto& e : kv_ev) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     HIPCHK(hipMalloc((void**)&kv_sink, 256));
