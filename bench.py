@@ -545,14 +545,14 @@ def main():
         "encoder_tflops": round(encoder_flops(dims) * enc_windows / (enc_ms * 1e-3) / 1e12, 1) if enc_ms else None,
         "roofline": {"bound": "hbm", "kernel": (f"k_proj1 whole-K projection, fused LayerNorm / epilogue ({rows} rows"
                                                 if p1 else f"k_proj split-K projection ({rows} rows")
-                                               + ", avg of the six per decoder layer)",
+                                               + f", avg of the {'five' if fused_q else 'six'} per decoder layer)",
                      "achieved": round(gbs(gemv_bytes, gemv_ms), 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(gbs(gemv_bytes, gemv_ms) / HBM_PEAK_GBS, 4),
                      "traffic": traffic, "bytes_per_launch": gemv_bytes, "ms_per_launch": round(gemv_ms, 5),
                      "timing": "HIP events around each launch inside eager decoder steps",
                      "launches_per_layer": 5 if fused_q else 6,
                      "ms_per_launch_back_to_back": round(gemv_b2b_ms, 5),
-                     "back_to_back_note": "time_stage 2: the six projections of each layer queued without their "
+                     "back_to_back_note": "time_stage 2: the layer's projections queued without their "
                                           "producers; on the k_proj1 path the non-deferred fc2 and the plain QKV "
                                           "LayerNorm prologue (the step itself defers fc2's residual)"},
         "roofline_overall": overall,
