@@ -74,6 +74,10 @@ struct XQPart {
   const float* ln_g = nullptr;
   const float* ln_b = nullptr;
   float ln_eps = 1e-5f;
+  // ... with the projection split over the pair's workgroups (k_xattn_seg QV 6): the partial
+  // queries [pair][XQ1_P][4][64] float4 and per pair {arrivals, departures} (zero between launches)
+  float* q_part = nullptr;
+  int* q_cnt = nullptr;
 };
 // the shapes the in-kernel query projection serves: fp16, n = 1280 (large-v3, turbo), <= 8
 // rows per window; the choice depends on the model and the beam group only, never on the
@@ -93,6 +97,7 @@ constexpr int XREC = 16 * 64 + 32;  // floats per segment record: O[16][64], m[1
 // step cross-attention (k_xattn_seg): one softmax partial per 64-key tile, at most
 // XS_NSP tiles per (window, head) pair (Tk <= 1536), at most XS_QP pairs per workgroup
 constexpr int XS_NSP = 24;
+constexpr int XQ1_P = 8;  // workgroups per pair of the split single-window query projection (k_xattn_seg QV 6)
 constexpr int XS_QP = 4;
 int xattn_seg_grid(int npair, int nsp, int smax);
 inline bool cross_attn_q_slabs(int z) { return z == 4 || z == 8 || z == 10; }

@@ -1983,6 +1983,134 @@ WH_DEV void xq_project(const XQPart& xq, int pa, int plast, int cnt, const int* 
   }
 }
 
+// QV 6 (round 6, the single-window step): the query projection split over the XQ1_P workgroups
+// of each (window, head) pair instead of computed whole by each of them (QV 3: every one of
+// the 240 workgroups ingested its head's 164 KB W_q slice before any tile, 6.1 -> 15.3 us).
+// The grid gives every workgroup nsp / XQ1_P tiles of ONE pair; workgroup kpart of the pair
+// computes the partial query over k-steps [kpart KS, kpart KS + KS) (KS = 2 QK / XQ1_P), stores
+// it write-through into xq.q_part, drains and counts it on the pair's arrival counter; the
+// query is the XQ1_P partials summed in kpart order + the bias (the same arithmetic in every
+// workgroup of the pair).  Roles: waves < cnt (the tile waves) issue their tile's K / V first
+// and wait at the barriers; waves 3-7 compute the LayerNorm of the window's rows (k_proj1's
+// arithmetic) into LDS; waves 4-7 (column tile c = wave - 4) run the partial projection; wave
+// 3 polls the counter (sc1 loads, bounded: a lost arrival ends the wait with a wrong query,
+// never a hang).  Every workgroup of the pair is resident at once (XQ1_P x npair <= 256
+// one-workgroup-per-CU launches: the launcher checks).  The last of the pair's workgroups to
+// read the partials re-arms both counters (departure count).
+template <typename T, int QK, int RR, typename PairWH, typename LoadKV>
+WH_DEV void xq_project_split(const XQPart& xq, int pa, int kpart, int cnt, const int* __restrict__ win_row0,
+                             const int* __restrict__ win_nrows, PairWH pair_wh, LoadKV load_kv, Frag<T> (&kA)[4][2],
+                             Frag<T> (&vA)[4][2], char* xst, T (*qs)[16][72], int* s_wnr, int* s_wr0) {
+  static_assert(sizeof(T) == 2, "fused query projection: fp16 contexts");
+  constexpr int N = QK * 64, KS = 2 * QK / XQ1_P, CPL = N / 256, XROWB = N * (int)sizeof(T) + 16;
+  static_assert((2 * QK) % XQ1_P == 0 && N % 256 == 0 && RR <= 10, "split geometry");
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = lane & 15, g = lane >> 4;
+  int wi, h;
+  pair_wh(pa, wi, h);
+  // the tile waves' K / V leave first (nothing of theirs waits on the query until the tiles)
+  if (wave < cnt) load_kv(wave, kA, vA);
+  const int nr = win_nrows[wi], r0 = win_row0[wi];
+  if (tid == 0) {
+    s_wnr[0] = nr;
+    s_wr0[0] = r0;
+  }
+  const bool pw = wave >= 4;  // projection waves: column tile c = wave - 4
+  const int c = wave - 4;
+  Frag<T> wf[KS];
+  if (pw) {  // W_q rows h*64 + 16c + r, k-steps kpart*KS .. + KS - 1
+    const T* wp = reinterpret_cast<const T*>(xq.qw) + (int64_t)(h * 64 + c * 16 + r) * N + kpart * KS * 32 + 8 * g;
+#pragma unroll
+    for (int s = 0; s < KS; ++s) frag_load_stream(wf[s], wp + s * 32);
+  }
+  // LayerNorm: waves 3..7 take rows wave - 3 and wave + 2 (rows past the window repeat its last)
+  if (wave >= 3) {
+    float4_t lg[CPL], lb[CPL];
+#pragma unroll
+    for (int i = 0; i < CPL; ++i) {
+      lg[i] = load4f(xq.ln_g + 4 * (lane + 64 * i));
+      lb[i] = load4f(xq.ln_b + 4 * (lane + 64 * i));
+    }
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const int row = wave - 3 + 5 * t;
+      if (row < RR) {
+        const float* xr = reinterpret_cast<const float*>(xq.qx) + (int64_t)(r0 + min(row, nr - 1)) * N;
+        float4_t lx[CPL];
+#pragma unroll
+        for (int i = 0; i < CPL; ++i) lx[i] = load4f(xr + 4 * (lane + 64 * i));
+        float sm = 0.f;
+#pragma unroll
+        for (int i = 0; i < CPL; ++i) sm += lx[i][0] + lx[i][1] + lx[i][2] + lx[i][3];
+        const float mean = wave_sum(sm) / (float)N;
+        float qv2 = 0.f;
+#pragma unroll
+        for (int i = 0; i < CPL; ++i)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float d = lx[i][e] - mean;
+            qv2 += d * d;
+          }
+        const float rstd = rsqrtf(wave_sum(qv2) / (float)N + xq.ln_eps);
+#pragma unroll
+        for (int i = 0; i < CPL; ++i) {
+          const float4_t v = lx[i];
+          store4(reinterpret_cast<T*>(xst + row * XROWB) + 4 * (lane + 64 * i), (v[0] - mean) * rstd * lg[i][0] + lb[i][0],
+                 (v[1] - mean) * rstd * lg[i][1] + lb[i][1], (v[2] - mean) * rstd * lg[i][2] + lb[i][2],
+                 (v[3] - mean) * rstd * lg[i][3] + lb[i][3]);
+        }
+      }
+    }
+  }
+  wh_lds_barrier();
+  XS_MARK(7);  // rows staged
+  const auto rq = wt_rsrc(xq.q_part);
+  const int pbase = pa * XQ1_P * 4 * 64 * 16;  // bytes: [pair][kpart][c][lane] float4
+  int* const arr = xq.q_cnt + 2 * pa;          // [pair]{arrivals, departures}
+  if (pw) {
+    float4_t acc = (float4_t){0.f, 0.f, 0.f, 0.f};
+    const char* xl = xst + min(r, RR - 1) * XROWB;
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      Frag<T> xf;
+      frag_load(xf, reinterpret_cast<const T*>(xl + ((kpart * KS + s) * 4 + g) * 16));
+      mfma_step(acc, wf[s], xf);
+    }
+    wt_store4(rq, pbase + ((kpart * 4 + c) * 64 + lane) * 16, acc);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's partial is written through
+    if (lane == 0) __hip_atomic_fetch_add(arr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  } else if (wave == 3) {
+    const auto ra = wt_rsrc(arr);
+    int v = 0;
+    for (int it = 0; it < (1 << 16); ++it) {  // (~65 ms: a normal wait is a few us)
+      v = (int)__builtin_amdgcn_raw_buffer_load_b32(ra, 0, 0, 16);
+      if (v >= 4 * XQ1_P) break;
+      __builtin_amdgcn_s_sleep(1);
+    }
+    (void)v;
+  }
+  wh_lds_barrier();  // wave 3 has seen every partial of the pair arrive
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // no instruction: keeps the loads below
+  if (pw) {
+    float4_t pv[XQ1_P];
+#pragma unroll
+    for (int j = 0; j < XQ1_P; ++j)
+      pv[j] = __builtin_bit_cast(float4_t, __builtin_amdgcn_raw_buffer_load_b128(rq, pbase + ((j * 4 + c) * 64 + lane) * 16, 0, 16));
+    float4_t q = pv[0];
+#pragma unroll
+    for (int j = 1; j < XQ1_P; ++j) q += pv[j];
+    q += load4f(xq.bias + h * 64 + c * 16 + 4 * g);
+    store4(&qs[0][r][c * 16 + 4 * g], q[0], q[1], q[2], q[3]);
+    if (wave == 4 && lane == 0) {
+      // every workgroup of the pair departs once it has read the partials; the last re-arms
+      if (__hip_atomic_fetch_add(arr + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == XQ1_P - 1) {
+        __hip_atomic_store(arr, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(arr + 1, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+  }
+  XS_MARK(8);  // query summed
+}
+
 template <typename T, int QZ, int RR, typename S = float, bool FULL = false, int QK = 0, int QV = 0>
 __global__ __launch_bounds__(512, 1) void k_xattn_seg(const T* __restrict__ q, int ldq, const T* ck, const T* cvt, int Tk,
                                                      int H, int npair, int nsp, const int* __restrict__ win_row0,
@@ -2112,8 +2240,12 @@ __global__ __launch_bounds__(512, 1) void k_xattn_seg(const T* __restrict__ q, i
     static_assert(XS_QF * RR * (QK * 64 * sizeof(T) + 16) + 2 * XS_QF * 4 * 64 * 16 + XS_QF * 256 <= sizeof(seg_o),
                   "X rows, K-half sums and biases in the partials' LDS");
     static_assert(XS_QF * 4 * 64 * 16 <= sizeof(seg_o), "K-half sums in the partials' LDS");
-    xq_project<T, QK, RR, QV>(xq, pa, plast, cnt, win_row0, win_nrows, pair_wh, load_kv, kA, vA, kB, vB,
-                              reinterpret_cast<char*>(&seg_o[0][0][0]), qs, s_wnr, s_wr0);
+    if constexpr (QV == 6)
+      xq_project_split<T, QK, RR>(xq, pa, (s0 - pa * nsp) / max(cnt, 1), cnt, win_row0, win_nrows, pair_wh, load_kv, kA,
+                                  vA, reinterpret_cast<char*>(&seg_o[0][0][0]), qs, s_wnr, s_wr0);
+    else
+      xq_project<T, QK, RR, QV>(xq, pa, plast, cnt, win_row0, win_nrows, pair_wh, load_kv, kA, vA, kB, vB,
+                                reinterpret_cast<char*>(&seg_o[0][0][0]), qs, s_wnr, s_wr0);
   } else {
   // FULL (the launcher: every workgroup holds >= 8 tiles, one per wave at least): the order
   // above; otherwise (few windows, <= 1 tile per wave) the first tile leaves first, as the
@@ -2183,7 +2315,9 @@ __global__ __launch_bounds__(512, 1) void k_xattn_seg(const T* __restrict__ q, i
   asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // LDS only
   XS_MARK(1);
 
-  if (QF && QV >= 1 && wave < cnt) {
+  if (QF && QV == 6) {
+    if (wave < cnt) tile(kA, vA, wave);  // (the launcher: <= NW tiles per workgroup)
+  } else if (QF && QV >= 1 && wave < cnt) {
     // (QV 1 / 2) kB / vB already hold tile wave + NW (clamped): the next tile is in flight on
     // entry, so each iteration refills the buffer it has just computed
     int i = wave;
@@ -2414,6 +2548,18 @@ void launch_cross_attn(const T* q, int ldq, const T* ck, const T* cv, int Tk, in
           // 2 tiles of ONE pair (nsp even): 12 workgroups per pair, merged through records
           if (nwin != 1 || !xq.ln_b || nsp % 2) {
             wh_set_launch_error("launch_cross_attn: in-kernel LayerNorm query is the single-window form");
+            return;
+          }
+          if (xq.q_part && xq.q_cnt) {
+            // QV 6: the projection split over the XQ1_P workgroups of each pair (all resident:
+            // one 512-thread workgroup per CU, npair x XQ1_P <= 256)
+            if (nsp % XQ1_P || nsp / XQ1_P > 8 || npair * XQ1_P > 256 || xq.max_rows > 10) {
+              wh_set_launch_error("launch_cross_attn: split query projection outside its shapes");
+              return;
+            }
+            k_xattn_seg<T, 0, 8, float, false, 20, 6><<<npair * XQ1_P, 512, 0, st>>>(
+                q, ldq, ck, cv, Tk, H, npair, nsp, win_row0, win_nrows, win_slot, win_stride, xq, out, ldo),
+                wh_launched("k_xattn_seg<qproj-split+ln>");
             return;
           }
           k_xattn_seg<T, 0, 8, float, false, 20, 3><<<npair * nsp / 2, 512, 0, st>>>(

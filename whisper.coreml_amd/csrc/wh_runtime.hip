@@ -227,6 +227,8 @@ struct Ctx : public wh_ctx {
   float* xs_rec = nullptr;   // step cross-attention segment records [pair][XS_NSP][XREC]
   float* x2_d = nullptr;     // k_proj1 path: second residual buffer (deferred residual ping-pong)
   int* xs_cnt = nullptr;     // and (window, head) arrival counters
+  float* xq1_part = nullptr; // single-window split query projection: partials [head][8][4][64] float4
+  int* xq1_cnt = nullptr;    // and {arrivals, departures} per head (zero between launches)
 
   // the step cross-attention's query / split arguments
   XQPart step_xq(int rows_per_window) const {
@@ -415,6 +417,7 @@ struct Ctx : public wh_ctx {
     addA((size_t)P1_SLABS * 256 * 4); addA((size_t)(4 * n / 16) * 4);  // k_proj1 split-K slabs + counters
     addA((size_t)Wcap * nh * XS_NSP * XREC * 4); addA((size_t)Wcap * nh * 4);  // cross-attention segment records
     addA((size_t)8 * n * 4);  // k_proj1 path (<= 8 rows, wh_proj.h P1_RMAX): the second residual buffer
+    addA((size_t)nh * XQ1_P * 4 * 64 * 16); addA((size_t)nh * 2 * 4);  // split query partials + counters
     addA((size_t)EKZ_TILES(n) * 65536); addA((size_t)EKZ_TILES(n) * 4 * 4);  // single-window encoder K halves
     HIPCHK(hipMalloc(&abase, ab));
     HIPCHK(hipMemset(abase, 0, ab));
@@ -454,8 +457,10 @@ struct Ctx : public wh_ctx {
     p1_slab = fa((size_t)P1_SLABS * 256); p1_cnt = ia(4 * n / 16);  // zeroed with the arena
     xs_rec = fa((size_t)Wcap * nh * XS_NSP * XREC); xs_cnt = ia((size_t)Wcap * nh);
     x2_d = fa((size_t)8 * n);
+    xq1_part = fa((size_t)nh * XQ1_P * 4 * 64 * 4); xq1_cnt = ia((size_t)nh * 2);  // zeroed with the arena
     ekz_slab = fa((size_t)EKZ_TILES(n) * 16384); ekz_cnt = ia((size_t)EKZ_TILES(n) * 4);  // zeroed with the arena
-    if (!fp_anc || !S.seed || !S.cand_idx || !S.lp_cnt || !S.lpw_cnt || !vs_cnt || !p1_cnt || !xs_cnt || !x2_d || !ekz_cnt)
+    if (!fp_anc || !S.seed || !S.cand_idx || !S.lp_cnt || !S.lpw_cnt || !vs_cnt || !p1_cnt || !xs_cnt || !x2_d || !ekz_cnt ||
+        !xq1_cnt)
       return fail(-3, "activation arena overflow");
     S.nw = Wcap; S.G = 1; S.ctx = CTX; S.hctx = HCTX; S.maxc = 16;
     HIPCHK(hipMalloc(&d_gmax, 64));
@@ -1119,7 +1124,7 @@ struct Ctx : public wh_ctx {
   std::string step_kernels(int n_win, int group) const override {
     const bool p1 = p1_active(n_win * group, n_win), h = sizeof(T) == 2;
     return std::string("proj=") + (p1 ? "k_proj1" : "k_proj") + ",xattn=k_xattn_seg" +
-           (!p1 && xq_proj_active(group) ? "<qproj>" : p1 && xq_proj1_active(group) ? "<qproj+ln>" : "") +
+           (!p1 && xq_proj_active(group) ? "<qproj>" : p1 && xq_proj1_active(group) ? (xq_proj1_mode() == 2 ? "<qproj-split+ln>" : "<qproj+ln>") : "") +
            ",self_attn=" +
            (p1 ? (h && self_attn_kco_on() ? "k_self_attn<kco>" : "k_self_attn")
                : h && group >= 2 && self_attn_grp_mode() ? "k_self_attn_grp"
@@ -1171,7 +1176,11 @@ struct Ctx : public wh_ctx {
         // round 6: no cross-q k_proj1 launch; the cross-attention normalises the window's
         // fp32 rows and projects its query itself
         xq.qx = xc; xq.qw = e.wqx; xq.bias = e.bqx; xq.ln_g = e.lnx_g; xq.ln_b = e.lnx_b; xq.ln_eps = 1e-5f;
-        if (xq_frag_on()) xq.qwf = e.wqx_f;
+        if (xq_proj1_mode() == 2) {
+          xq.q_part = xq1_part; xq.q_cnt = xq1_cnt;
+        } else if (xq_frag_on()) {
+          xq.qwf = e.wqx_f;
+        }
       } else {
         g = GemmArgs();
         g.W = e.wqx; g.bias = e.bqx; g.M = R; g.N = n; g.K = n;
@@ -1554,13 +1563,15 @@ struct Ctx : public wh_ctx {
   // window 240 workgroups each ingest the 164 KB W_q slice of their head before any tile can
   // run, and the cross-attention launch grows 6.1 -> 17.4 us against the 5-7 us the cross-q
   // k_proj1 launch and its boundary cost (turbo step graph 0.274 -> 0.300 ms)
-  static bool xq_proj1_on() {
-    static const bool on = [] {
+  // WHISPER_HIP_XQP1=2: the projection split over each pair's 8 workgroups (k_xattn_seg QV 6)
+  static int xq_proj1_mode() {
+    static const int v = [] {
       const char* e = tune_env("WHISPER_HIP_XQP1");
-      return e && e[0] == '1';
+      return e ? atoi(e) : 0;
     }();
-    return on;
+    return v;
   }
+  static bool xq_proj1_on() { return xq_proj1_mode() > 0; }
   bool xq_proj1_active(int rows_per_window) const { return xq_proj1_on() && xq_proj_active(rows_per_window); }
 
   // WHISPER_HIP_EAGER=1 launches the step kernels directly instead of replaying the
