@@ -1953,6 +1953,9 @@ struct Ctx : public wh_ctx {
               if (xq_frag_on()) xq.qwf = e.wqx_f;
               if (p1_active(R, cur_nwin)) {
                 xq.qx = x_d; xq.ln_g = e.lnx_g; xq.ln_b = e.lnx_b;
+                if (xq_proj1_mode() == 2) {  // the split projection, as the step runs it
+                  xq.q_part = xq1_part; xq.q_cnt = xq1_cnt; xq.qwf = nullptr;
+                }
               } else {
                 xq.qx = xn_d;
               }
