@@ -4,4 +4,4 @@ set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out
 rm -f gpurun_out/margins.jsonl
-bash profiles/gpu_session.sh r6g tests smoke cfg3 cfg2
+bash profiles/gpu_session.sh r6h tests smoke cfg3 cfg2
